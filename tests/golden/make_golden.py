@@ -1,0 +1,179 @@
+"""Generate the golden vectors that pin the oracle to the reference.
+
+Run in the build container (where /root/reference exists):
+
+    python tests/golden/make_golden.py
+
+It imports the REFERENCE itself (read-only, CPU, torch 2.10.0) with a stub for the
+missing ``termcolor`` package, drives its hot-path entry points with the FakeLM
+banks of tests/fakelm.py under fixed ``torch.manual_seed`` seeds, and writes:
+
+* ``spec_loops.json``   — ``sampling.speculative_generate`` outputs (batch-1 rule A8)
+* ``engine_loops.json`` — ``engine.infer_engine.batch_speculative_generate`` outputs (rule A10)
+* ``processors.safetensors`` — ``utils.logits_processor`` probabilities on small rows
+* ``caching.json``      — ``utils.caching.prune_tuple_cache`` shapes
+
+Only data is committed (inputs are regenerated from seeds + checked by digest);
+no reference source travels.  The GPU box never runs this script.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import types
+from types import SimpleNamespace
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+sys.path.insert(0, os.path.dirname(HERE))           # tests/ (fakelm)
+from fakelm import make_pair, bank_digest, likely_tokens   # noqa: E402
+
+SPEC_CASES = [
+    # name, V, dtype, gamma, processor(kind, T, k, p), gen_len, eos, skip_adj, seeds
+    ("greedy_g4_bf16", 4096, "bf16", 4, ("greedy", 1.0, 0, 1.0), 40, [1], False, [0, 1]),
+    ("greedy_g1_bf16", 4096, "bf16", 1, ("greedy", 1.0, 0, 1.0), 24, [1], False, [0]),
+    ("greedy_g8_bf16", 4096, "bf16", 8, ("greedy", 1.0, 0, 1.0), 40, [1], False, [0]),
+    ("multi_t1_g4_bf16", 4096, "bf16", 4, ("multinomial", 1.0, 0, 1.0), 40, [1], False, [0, 1, 2]),
+    ("multi_t07_g4_bf16", 4096, "bf16", 4, ("multinomial", 0.7, 0, 1.0), 40, [1], False, [0, 1]),
+    ("multi_t1_g8_bf16", 4096, "bf16", 8, ("multinomial", 1.0, 0, 1.0), 40, [1], False, [3]),
+    ("multi_t1_g4_bf16_skipadj", 4096, "bf16", 4, ("multinomial", 1.0, 0, 1.0), 40, [1], True, [0]),
+    ("multi_t1_g4_bf16_eos", 4096, "bf16", 4, ("multinomial", 1.0, 0, 1.0), 60, "likely", False,
+     [0, 1, 2, 3]),
+    ("greedy_g4_bf16_eos", 4096, "bf16", 4, ("greedy", 1.0, 0, 1.0), 60, "likely", False, [0, 1]),
+    ("topk20_g4_bf16", 4096, "bf16", 4, ("topk", 1.0, 20, 1.0), 40, [1], False, [0, 1]),
+    ("topk50_t08_g4_bf16", 4096, "bf16", 4, ("topk", 0.8, 50, 1.0), 40, [1], False, [0]),
+    ("nucleus09_g4_bf16", 4096, "bf16", 4, ("nucleus", 1.0, 0, 0.9), 40, [1], False, [0, 1]),
+    ("nucleus08_t07_g4_bf16", 4096, "bf16", 4, ("nucleus", 0.7, 0, 0.8), 40, [1], False, [0]),
+    ("topknucleus_g4_bf16", 4096, "bf16", 4, ("topknucleus", 1.0, 50, 0.9), 40, [1], False, [0]),
+    ("greedy_g4_fp32", 4096, "fp32", 4, ("greedy", 1.0, 0, 1.0), 40, [1], False, [0]),
+    ("multi_t1_g4_fp32", 4096, "fp32", 4, ("multinomial", 1.0, 0, 1.0), 40, [1], False, [0, 1]),
+    ("nucleus09_g4_fp32", 4096, "fp32", 4, ("nucleus", 1.0, 0, 0.9), 32, [1], False, [0]),
+    ("gpt2like_greedy_g4_fp32", 50257, "fp32", 4, ("greedy", 1.0, 0, 1.0), 32, [50256], False, [0]),
+    ("llama_greedy_g4_bf16", 128256, "bf16", 4, ("greedy", 1.0, 0, 1.0), 24, [128001, 128009], False, [0]),
+    ("llama_multi_g4_bf16", 128256, "bf16", 4, ("multinomial", 1.0, 0, 1.0), 24, [128001, 128009], False, [0]),
+]
+
+# The engine re-feeds the last prompt token to the drafter after its prefill (engine/infer_engine.py:206,231),
+# so drafter and target see it at different positions; pos_mult=0 banks (logits depend on the token only)
+# keep their distributions aligned so the accept branch is exercised.
+ENGINE_CASES = [
+    # name, V, dtype, B, gamma, gen_len, end_tokens, seeds[, pos_mult]
+    ("b1_g4_bf16_pos7", 4096, "bf16", 1, 4, 32, [1], [0], 7),
+    ("b1_g4_bf16", 4096, "bf16", 1, 4, 32, [1], [0, 1]),
+    ("b1_g4_fp32", 4096, "fp32", 1, 4, 32, [1], [0]),
+    ("b4_g4_fp32", 4096, "fp32", 4, 4, 32, [1], [0, 1]),
+    ("b6_g4_fp32_eos", 2048, "fp32", 6, 4, 40, "likely", [0, 1]),
+    ("b6_g1_fp32", 2048, "fp32", 6, 1, 16, [1], [0]),
+    ("b5_g3_fp32_ragged", 2048, "fp32", 5, 3, 17, "likely", [2]),
+    ("b1_g4_bf16_eos", 4096, "bf16", 1, 4, 40, "likely", [0, 1, 2]),
+    ("b4_g4_bf16_refcrash", 4096, "bf16", 4, 4, 16, [1], [0]),
+    ("llama_b2_g4_fp32", 128256, "fp32", 2, 4, 12, [128001, 128009], [0]),
+]
+
+DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
+
+
+def _import_reference():
+    sys.modules.setdefault("termcolor", types.SimpleNamespace(colored=lambda s, *a, **k: s, cprint=print))
+    sys.path.insert(0, REF)
+    from sampling.speculative_decoding import speculative_generate      # noqa
+    from utils import logits_processor as lp                             # noqa
+    from utils.caching import prune_tuple_cache                          # noqa
+    from engine.infer_engine import batch_speculative_generate           # noqa
+    return speculative_generate, lp, prune_tuple_cache, batch_speculative_generate
+
+
+def prompt_for(V: int, seed: int, length: int = 8, batch: int = 1):
+    g = torch.Generator().manual_seed(10_000 + seed)
+    return torch.randint(3, V, (batch, length), generator=g)
+
+
+def make_processor(lp, kind, T, k, p):
+    return {"greedy": lambda: lp.GreedyProcessor(T),
+            "multinomial": lambda: lp.MultinomialProcessor(T),
+            "topk": lambda: lp.TopKProcessor(T, k),
+            "nucleus": lambda: lp.NucleusProcessor(T, p),
+            "topknucleus": lambda: lp.TopKNucleusProcessor(T, k, p)}[kind]()
+
+
+def main():
+    speculative_generate, lp, prune_tuple_cache, batch_speculative_generate = _import_reference()
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+
+    spec = {}
+    for name, V, dt, gamma, (kind, T, k, p), gen_len, eos, skip, seeds in SPEC_CASES:
+        target, drafter = make_pair(V, dtype=DT[dt])
+        if eos == "likely":
+            eos = likely_tokens(target)
+        for seed in seeds:
+            prompt = prompt_for(V, seed)[0].tolist()
+            torch.manual_seed(seed)
+            out, rate = speculative_generate(
+                prompt, drafter, target, gamma=gamma, logits_processor=make_processor(lp, kind, T, k, p),
+                max_gen_len=gen_len, eos_tokens_id=eos if len(eos) > 1 else eos[0], pad_token_id=0,
+                skip_sample_adjustment=skip)
+            spec[f"{name}/s{seed}"] = dict(
+                vocab=V, dtype=dt, gamma=gamma, processor=dict(kind=kind, temperature=T, top_k=k, top_p=p),
+                max_gen_len=gen_len, eos=eos, skip_sample_adjustment=skip, seed=seed, prompt=prompt,
+                target_digest=bank_digest(target), drafter_digest=bank_digest(drafter),
+                tokens=out, acceptance_rate=float(rate))
+            print(name, seed, len(out), rate, flush=True)
+    with open(os.path.join(HERE, "spec_loops.json"), "w") as f:
+        json.dump(spec, f, indent=1)
+
+    eng = {}
+    for name, V, dt, B, gamma, gen_len, ends, seeds, *pm in ENGINE_CASES:
+        pos_mult = pm[0] if pm else 0
+        target, drafter = make_pair(V, dtype=DT[dt], pos_mult=pos_mult)
+        if ends == "likely":
+            ends = likely_tokens(target)
+        for seed in seeds:
+            ids = prompt_for(V, seed, batch=B)
+            mask = torch.ones_like(ids)
+            ctx = SimpleNamespace(drafter=drafter, target=target, gamma=gamma, gen_len=gen_len,
+                                  end_tokens=ends, target_device="cpu")
+            torch.manual_seed(seed)
+            rec = dict(vocab=V, dtype=dt, batch=B, gamma=gamma, gen_len=gen_len, end_tokens=ends, seed=seed,
+                       pos_mult=pos_mult,
+                       prompt=ids.tolist(), target_digest=bank_digest(target),
+                       drafter_digest=bank_digest(drafter))
+            try:
+                outs, rates = batch_speculative_generate(ctx, ids, mask, B)
+                rec.update(outputs=[o.tolist() for o in outs], rates=[float(r) for r in rates], raised=None)
+            except Exception as e:  # the reference's bf16 B>=2 index_put crash (engine/infer_engine.py:254)
+                rec.update(outputs=None, rates=None, raised=f"{type(e).__name__}: {e}")
+            eng[f"{name}/s{seed}"] = rec
+            print(name, seed, rec["raised"] or [len(o) for o in rec["outputs"]], flush=True)
+    with open(os.path.join(HERE, "engine_loops.json"), "w") as f:
+        json.dump(eng, f, indent=1)
+
+    # processors on small rows
+    from safetensors.torch import save_file
+    tens = {}
+    meta = {}
+    g = torch.Generator().manual_seed(7)
+    base = torch.randn(3, 1024, generator=g) * 3
+    configs = [("greedy", 1.0, 0, 1.0), ("multinomial", 0.7, 0, 1.0), ("topk", 1.0, 20, 1.0),
+               ("topk", 0.8, 50, 1.0), ("nucleus", 1.0, 0, 0.9), ("nucleus", 0.7, 0, 0.5),
+               ("topknucleus", 1.0, 50, 0.9), ("topknucleus", 1.3, 10, 0.95)]
+    for dt in ("bf16", "fp32"):
+        x = base.to(DT[dt])
+        tens[f"logits_{dt}"] = x.contiguous()
+        for i, (kind, T, k, p) in enumerate(configs):
+            proc = make_processor(lp, kind, T, k, p)
+            tens[f"probs_{dt}_{i}"] = proc(x.clone()).contiguous()
+            meta[f"{dt}_{i}"] = f"{kind},{T},{k},{p}"
+    save_file(tens, os.path.join(HERE, "processors.safetensors"), metadata=meta)
+
+    # prune_tuple_cache shapes
+    cache = tuple((torch.zeros(1, 2, 10, 4), torch.zeros(1, 2, 10, 4)) for _ in range(3))
+    shapes = {str(k): [list(t.shape) for t in prune_tuple_cache(cache, k)[0]] for k in (1, 3, 5)}
+    with open(os.path.join(HERE, "caching.json"), "w") as f:
+        json.dump(shapes, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
