@@ -1,0 +1,211 @@
+/*
+ * specdec.h — C ABI of the MI355X-native speculative verify/accept path.
+ *
+ * The reference (dadiaokua/speculative-decoding) is pure Python and has no FFI; this
+ * library sits under the Python entry points it exposes for the hot path, which keep
+ * their signatures (the specdec_amd Python package):
+ *
+ *   sd_verify      replaces the per-step verify block of
+ *                    sampling/speculative_decoding.py:129-187   (rule SD_RULE_SPEC,   "A8")
+ *                    engine/infer_engine.py:265-336             (rule SD_RULE_ENGINE, "A10")
+ *                  including the processors it calls (utils/logits_processor.py:13-103),
+ *                  max_fn (sampling/speculative_decoding.py:10-19) and the prune lengths fed
+ *                  to utils/caching.py:6-24 (sampling/speculative_decoding.py:163-165).
+ *   sd_sample      replaces LogitsProcessor.__call__ + .sample on the drafter / first-target
+ *                  rows (sampling/speculative_decoding.py:95-96,120-123; engine/infer_engine.py:241-246).
+ *   sd_mt19937_*   host-side mirror of torch's CPU generator (ATen mt19937) that feeds the
+ *                  "stream" noise mode, so GPU results equal the reference's under a fixed
+ *                  torch.manual_seed (torch.rand: engine/infer_engine.py:305,
+ *                  sampling/speculative_decoding.py:139; torch.multinomial's Exp(1) noise).
+ *
+ * Conventions: all tensor pointers are device pointers (hipMalloc / torch CUDA memory);
+ * the vocab axis has unit stride; other strides are in ELEMENTS.  Every entry point
+ * returns SD_OK or a negative sd_status, never aborts, never allocates, never syncs the
+ * host; kernels are enqueued on `stream` (a hipStream_t, passed as void*).  Per-row
+ * failures (e.g. an all-zero residual under multinomial, which makes torch raise) are
+ * reported in `row_status`, read back by the caller.
+ */
+#ifndef SPECDEC_H
+#define SPECDEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SD_ABI_VERSION 1
+#define SD_MAX_GAMMA 16
+
+typedef enum {
+    SD_OK = 0,
+    SD_ERR_INVALID = -1,      /* bad argument (null pointer, bad shape, bad enum)        */
+    SD_ERR_WORKSPACE = -2,    /* workspace too small (see sd_*_workspace_size)            */
+    SD_ERR_LAUNCH = -3,       /* hipLaunchKernel / hip runtime error                      */
+    SD_ERR_UNSUPPORTED = -4,  /* combination not implemented                              */
+} sd_status;
+
+typedef enum { SD_F32 = 0, SD_BF16 = 1, SD_F16 = 2 } sd_dtype;
+
+/* utils/logits_processor.py: GreedyProcessor :26, MultinomialProcessor :39, TopKProcessor :52,
+ * NucleusProcessor :66, TopKNucleusProcessor :84.                                          */
+typedef enum {
+    SD_PROC_GREEDY = 0,
+    SD_PROC_MULTINOMIAL = 1,
+    SD_PROC_TOPK = 2,
+    SD_PROC_NUCLEUS = 3,
+    SD_PROC_TOPK_NUCLEUS = 4,
+} sd_proc_kind;
+
+typedef struct {
+    int32_t kind;         /* sd_proc_kind                       */
+    float temperature;    /* LogitsProcessor.temperature        */
+    int32_t top_k;        /* TopK*.top_k                         */
+    float top_p;          /* Nucleus*.top_p                      */
+} sd_processor;
+
+typedef enum {
+    SD_RULE_SPEC = 0,     /* sampling/speculative_decoding.py:139-171: accept iff r <= p/q (fp32),
+                             bonus sample on full accept, (p-q)+ residual on reject           */
+    SD_RULE_ENGINE = 1,   /* engine/infer_engine.py:287-336: accept iff u < min(1,p/q) (fp64),
+                             q<=0 accepts, eos ends the row, no bonus, residual on reject     */
+} sd_rule;
+
+typedef enum {
+    SD_NOISE_STREAM = 0,  /* words[] = mt19937 outputs of torch's CPU generator (parity mode) */
+    SD_NOISE_PHILOX = 1,  /* in-kernel Philox4x32-10 keyed by seed, counter offset (perf mode) */
+} sd_noise_mode;
+
+typedef struct {
+    int32_t mode;            /* sd_noise_mode                                                 */
+    const uint32_t* words;   /* STREAM: device buffer of generator words, consumed from [0]   */
+    int64_t n_words;         /* STREAM: capacity; overrun => row_status SD_ROW_NOISE_OVERRUN  */
+    uint64_t seed;           /* PHILOX: key                                                   */
+    uint64_t offset;         /* PHILOX: per-call counter offset (caller advances it)          */
+} sd_noise;
+
+/* row_status bits */
+#define SD_ROW_DONE           0x1   /* the row was processed                                  */
+#define SD_ROW_STOP_IN_DRAFTS 0x2   /* SPEC: an accepted draft is a stop token: the reference
+                                       returns before sampling (speculative_decoding.py:150-155);
+                                       stop_index holds its draft position                   */
+#define SD_ROW_FINISHED       0x4   /* ENGINE: the row hit an end token (infer_engine.py:310,328) */
+#define SD_ROW_RESIDUAL       0x8   /* x was drawn from the (p-q)+ residual                    */
+#define SD_ROW_BONUS          0x10  /* x was drawn from the bonus row (full accept, SPEC)      */
+#define SD_ROW_FALLBACK_P     0x20  /* ENGINE: residual mass <= 1e-12, x drawn from p (:319-321);
+                                       SPEC skip_sample_adjustment: x drawn from p_n (:169-170) */
+#define SD_ROW_INVALID_DIST   0x40  /* multinomial over NaN/zero mass: torch raises RuntimeError */
+#define SD_ROW_NOISE_OVERRUN  0x80  /* STREAM noise buffer too short                           */
+#define SD_ROW_NUCLEUS_INEXACT 0x100 /* nucleus cut computed where fp32 cumsum rounding could not
+                                       be reproduced exactly           */
+
+typedef struct {
+    /* shape */
+    int32_t batch;               /* B                                                         */
+    int32_t gamma;               /* γ' (drafts verified this step), 1..SD_MAX_GAMMA           */
+    int32_t vocab;               /* V                                                         */
+    int32_t rule;                /* sd_rule                                                   */
+
+    /* target logits: rows t = 0..gamma (gamma+1 rows; row gamma is the bonus row, read only
+       under SD_RULE_SPEC).  Row t of sequence b is target_rows[t] + b * target_stride_b.     */
+    const void* target_rows[SD_MAX_GAMMA + 1];
+    int64_t target_stride_b;
+    int32_t target_dtype;        /* sd_dtype                                                  */
+
+    /* drafter: rows d = 0..gamma-1; logits (processed with draft_proc) or, when
+       draft_is_probs, fp32 probabilities (the reference's q buffer).                         */
+    const void* draft_rows[SD_MAX_GAMMA];
+    int64_t draft_stride_b;
+    int32_t draft_dtype;
+    int32_t draft_is_probs;
+
+    const int64_t* draft_tokens; /* [B, >=gamma] drafted ids                                  */
+    int64_t draft_tokens_stride_b;
+
+    sd_processor target_proc;    /* SPEC: the loop's logits_processor; ENGINE: plain softmax  */
+    sd_processor draft_proc;
+
+    int32_t skip_sample_adjustment;  /* SPEC: sample from p_n instead of max_fn(p_n - q_n)    */
+    const int64_t* stop_tokens;      /* device [n_stop] eos ids (SPEC stop scan / ENGINE end)  */
+    int32_t n_stop;
+
+    const uint8_t* active;       /* ENGINE: [B] rows still generating (nullable = all)        */
+
+    sd_noise noise;
+
+    /* outputs, device, [B] */
+    int32_t* n_accepted;         /* accepted drafts n                                         */
+    int64_t* next_token;         /* token written at position cur+n (-1 if none)              */
+    float* resample_mass;        /* Σ (p_n - q_n)+ when a residual was formed, else NaN        */
+    int32_t* prune_drafter;      /* SPEC: γ'-n on reject, else 0 (utils/caching.py input)      */
+    int32_t* prune_target;       /* SPEC: γ'-n+1 on reject, else 0                            */
+    int32_t* stop_index;         /* SPEC: draft position of the first accepted stop token, -1  */
+    int32_t* row_status;         /* SD_ROW_* bits                                             */
+    int64_t* words_used;         /* STREAM: [1] words consumed by this call (nullable)         */
+
+    /* optional in-place engine state (ENGINE rule; nullable): applies
+       engine/infer_engine.py:307-336 on the device — generated[b, step+n] = x on reject,
+       zero the tail, finished[b] |= end token, accepted[b] += n.                             */
+    int64_t* generated;          /* [B, gen_len]                                              */
+    int64_t generated_stride_b;
+    int32_t step;
+    uint8_t* finished;           /* [B]                                                       */
+    int64_t* accepted_count;     /* [B]                                                       */
+
+    void* workspace;
+    size_t workspace_bytes;
+} sd_verify_args;
+
+typedef struct {
+    int32_t rows;                /* R rows sampled independently                               */
+    int32_t vocab;
+    const void* logits;          /* row r at logits + r * stride_r                            */
+    int64_t stride_r;
+    int32_t dtype;
+    sd_processor proc;
+    sd_noise noise;              /* STREAM: torch.multinomial on [R, V]: 2 words per element   */
+    int64_t* tokens;             /* [R] sampled ids (token r at tokens[r * tokens_stride])     */
+    int64_t tokens_stride;
+    float* token_prob;           /* [R] processed probability of the sampled id (nullable)     */
+    int32_t* row_status;         /* [R] (nullable)                                             */
+    int64_t* words_used;         /* [1] (nullable)                                             */
+    void* workspace;
+    size_t workspace_bytes;
+} sd_sample_args;
+
+/* LogitsProcessor.__call__ (utils/logits_processor.py:13-15) materialised: probs = softmax(_process(l)/T)
+ * in the logits dtype, row r written at probs + r * probs_stride_r.                        */
+typedef struct {
+    int32_t rows;
+    int32_t vocab;
+    const void* logits;
+    int64_t stride_r;
+    int32_t dtype;
+    sd_processor proc;
+    void* probs;
+    int64_t probs_stride_r;
+    void* workspace;
+    size_t workspace_bytes;
+} sd_probs_args;
+
+int32_t sd_abi_version(void);
+const char* sd_status_string(int32_t status);
+
+size_t sd_verify_workspace_size(int32_t batch, int32_t gamma, int32_t vocab);
+int32_t sd_verify(const sd_verify_args* args, void* stream);
+
+size_t sd_sample_workspace_size(int32_t rows, int32_t vocab);
+int32_t sd_sample(const sd_sample_args* args, void* stream);
+
+size_t sd_probs_workspace_size(int32_t rows, int32_t vocab);
+int32_t sd_probs(const sd_probs_args* args, void* stream);
+
+/* Host side: torch CPU generator state (torch.Generator.get_state(), 5056 bytes) <-> words. */
+int32_t sd_mt19937_fill(const uint8_t* torch_state, size_t state_len, uint32_t* out, int64_t n);
+int32_t sd_mt19937_advance(uint8_t* torch_state, size_t state_len, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPECDEC_H */

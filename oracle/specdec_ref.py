@@ -73,6 +73,10 @@ class Processor:
     temperature: float = 1.0
     top_k: int = 0
     top_p: float = 1.0
+    # Nucleus ties: the reference sorts with torch.sort(stable=False) (libstdc++ introsort on
+    # CPU), so WHICH of several equal logits at the cut survive is implementation-defined.
+    # stable_ties=True keeps them lowest-index first (the HIP kernel's rule; same count).
+    stable_ties: bool = False
 
     @property
     def stochastic(self) -> bool:
@@ -86,30 +90,44 @@ def _mask_below_kth(x: torch.Tensor, top_k: int) -> torch.Tensor:
     return x.masked_fill(x < kth, NEG_FILL)
 
 
-def _mask_outside_nucleus(x: torch.Tensor, top_p: float) -> torch.Tensor:
+def softmax(x: torch.Tensor, exact: bool = False) -> torch.Tensor:
+    """F.softmax in x's dtype; exact=True computes it in fp64 and rounds once to the dtype.
+
+    torch-CPU's own fp32 softmax sums exp() with vector-lane sequential accumulators: at
+    V=128256 its normaliser carries a ~4e-6 relative error, which moves ~0.5 % of the bf16
+    probabilities by one ulp.  The exact variant is the ideal value
+    the HIP kernels are measured against for floating-point quantities.
+    """
+    if not exact:
+        return F.softmax(x, dim=-1)
+    return F.softmax(x.double(), dim=-1).to(x.dtype)
+
+
+def _mask_outside_nucleus(x: torch.Tensor, top_p: float, exact: bool = False,
+                          stable: bool = False) -> torch.Tensor:
     # utils/logits_processor.py:73-81 (and :96-102): sort desc, cumsum(softmax) at T=1,
     # shift the removal mask right by one, always keep rank 0, unsort.
-    vals, order = torch.sort(x, descending=True)
-    csum = torch.cumsum(F.softmax(vals, dim=-1), dim=-1)
+    vals, order = torch.sort(x, descending=True, stable=stable)
+    csum = torch.cumsum(softmax(vals, exact), dim=-1)
     drop = torch.zeros_like(csum, dtype=torch.bool)
     drop[..., 1:] = (csum > top_p)[..., :-1]
     vals = vals.masked_fill(drop, NEG_FILL)
     return torch.gather(vals, -1, order.argsort(-1))
 
 
-def processed_logits(logits: torch.Tensor, proc: Processor) -> torch.Tensor:
+def processed_logits(logits: torch.Tensor, proc: Processor, exact: bool = False) -> torch.Tensor:
     """``LogitsProcessor._process`` on a copy (the reference's top-k mutates in place)."""
     x = logits.clone()
     if proc.kind in ("topk", "topknucleus"):
         x = _mask_below_kth(x, proc.top_k)
     if proc.kind in ("nucleus", "topknucleus"):
-        x = _mask_outside_nucleus(x, proc.top_p)
+        x = _mask_outside_nucleus(x, proc.top_p, exact, proc.stable_ties)
     return x
 
 
-def process(logits: torch.Tensor, proc: Processor) -> torch.Tensor:
+def process(logits: torch.Tensor, proc: Processor, exact: bool = False) -> torch.Tensor:
     """``LogitsProcessor.__call__`` (utils/logits_processor.py:13-15): softmax(_process(l) / T)."""
-    return F.softmax(processed_logits(logits, proc) / proc.temperature, dim=-1)
+    return softmax(processed_logits(logits, proc, exact) / proc.temperature, exact)
 
 
 def multinomial(probs: torch.Tensor, E: torch.Tensor) -> torch.Tensor:
@@ -149,7 +167,7 @@ class SpecStep:
 
 
 def spec_accept(target_rows: torch.Tensor, q: torch.Tensor, draft_ids: Sequence[int],
-                proc: Processor, r: torch.Tensor) -> Tuple[int, torch.Tensor]:
+                proc: Processor, r: torch.Tensor, exact: bool = False) -> Tuple[int, torch.Tensor]:
     """Accept test of ``speculative_generate`` (sampling/speculative_decoding.py:135-145).
 
     target_rows: [>=γ', V] target logits starting at row cur-1 of Mp.logits (:135)
@@ -158,7 +176,7 @@ def spec_accept(target_rows: torch.Tensor, q: torch.Tensor, draft_ids: Sequence[
     Returns (n, p) with p = processed target probs [1, γ', V].
     """
     g = q.shape[0]
-    p = process(target_rows[:g].unsqueeze(0), proc)              # :135-136
+    p = process(target_rows[:g].unsqueeze(0), proc, exact)       # :135-136
     frac = p / q.unsqueeze(0)                                      # :140 (bf16 / fp32 -> fp32)
     for i in range(g):                                             # :141-145
         if bool(r[i] > frac[0, i, int(draft_ids[i])]):
@@ -168,22 +186,28 @@ def spec_accept(target_rows: torch.Tensor, q: torch.Tensor, draft_ids: Sequence[
 
 def spec_resample(target_rows: torch.Tensor, q: torch.Tensor, p: torch.Tensor, n: int,
                   proc: Processor, E: Optional[torch.Tensor],
-                  skip_sample_adjustment: bool = False) -> SpecStep:
+                  skip_sample_adjustment: bool = False, exact: bool = False) -> SpecStep:
     """Bonus sample / (p-q)+ residual resample (sampling/speculative_decoding.py:158-171).
 
     E: [V] fp32 Exp(1) noise of the final multinomial (ignored for greedy).
+    exact: probabilities from the fp64 softmax and the residual mass summed in fp64.
     """
     g = q.shape[0]
     mass = float("nan")
     if n == g:                                                     # :158-160 bonus row
-        p_p = process(target_rows[g:g + 1], proc)
+        p_p = process(target_rows[g:g + 1], proc, exact)
         kd = kt = 0
     else:
         kd, kt = g - n, g - n + 1                                  # :163-165
         if not skip_sample_adjustment:                             # :167-168
             diff = p[..., n, :] - q[n, :]
-            mass = float(torch.where(diff > 0, diff, torch.zeros_like(diff)).sum())
-            p_p = max_fn(diff)
+            pos = torch.where(diff > 0, diff, torch.zeros_like(diff))
+            if exact:
+                mass = float(pos.double().sum())
+                p_p = pos / torch.tensor(mass, dtype=torch.float32)
+            else:
+                mass = float(pos.sum())
+                p_p = max_fn(diff)
         else:                                                      # :169-170
             p_p = p[..., n, :]
     if proc.stochastic:
@@ -193,10 +217,11 @@ def spec_resample(target_rows: torch.Tensor, q: torch.Tensor, p: torch.Tensor, n
     return SpecStep(n, x, mass, kd, kt)
 
 
-def spec_verify_step(target_rows, q, draft_ids, proc, r, E, skip_sample_adjustment=False) -> SpecStep:
+def spec_verify_step(target_rows, q, draft_ids, proc, r, E, skip_sample_adjustment=False,
+                     exact=False) -> SpecStep:
     """spec_accept + spec_resample on explicit noise (the kernel-level unit of the A8 rule)."""
-    n, p = spec_accept(target_rows, q, draft_ids, proc, r)
-    return spec_resample(target_rows, q, p, n, proc, E, skip_sample_adjustment)
+    n, p = spec_accept(target_rows, q, draft_ids, proc, r, exact)
+    return spec_resample(target_rows, q, p, n, proc, E, skip_sample_adjustment, exact)
 
 
 # --------------------------------------------------------------------------
@@ -206,7 +231,7 @@ def speculative_generate(inputs: List[int], drafter, target, gamma: int = 5,
                          proc: Processor = Processor(), max_gen_len: int = 40,
                          eos_tokens_id: Union[int, List[int]] = 1, pad_token_id: int = 0,
                          skip_sample_adjustment: bool = False, first_target: bool = True,
-                         noise: Optional[TorchNoise] = None) -> Tuple[List[int], float]:
+                         noise: Optional[TorchNoise] = None, exact: bool = False) -> Tuple[List[int], float]:
     noise = noise or TorchNoise()
     stops = eos_tokens_id if isinstance(eos_tokens_id, list) else [eos_tokens_id]
     accepted = speculated = 0.0                                    # :71
@@ -220,7 +245,7 @@ def speculative_generate(inputs: List[int], drafter, target, gamma: int = 5,
     cur = plen
     if first_target:                                               # :84-103
         logits = target(input_ids=ids[..., :cur], past_key_values=None, use_cache=False).logits
-        t = int(sample(process(logits[..., -1, :], proc), proc, noise).reshape(-1)[0])
+        t = int(sample(process(logits[..., -1, :], proc, exact), proc, noise).reshape(-1)[0])
         ids[0, cur] = t
         cur += 1
         if t in stops:
@@ -230,21 +255,21 @@ def speculative_generate(inputs: List[int], drafter, target, gamma: int = 5,
         q = torch.zeros((g, V), dtype=torch.float32)
         for k in range(g):                                         # :112-124
             dl = drafter(input_ids=ids[..., :cur + k], past_key_values=None, use_cache=False).logits
-            probs = process(dl[..., -1, :], proc)
+            probs = process(dl[..., -1, :], proc, exact)
             q[k] = probs[0].float()
             ids[0, cur + k] = int(sample(probs, proc, noise).reshape(-1)[0])
         speculated += g
         logits = target(input_ids=ids[..., :cur + g], past_key_values=None, use_cache=False).logits
         rows = logits[0, cur - 1:cur + g, :]                       # :135 + bonus row :159
         r = noise.uniform(g)                                       # :139
-        n, p = spec_accept(rows, q, ids[0, cur:cur + g].tolist(), proc, r)
+        n, p = spec_accept(rows, q, ids[0, cur:cur + g].tolist(), proc, r, exact)
         accepted += n                                              # :147
         hit = [j for j in range(n) if int(ids[0, cur + j]) in stops]   # :150-155
         if hit:
             return ids[0, plen:cur + hit[0] + 1].tolist(), accepted / speculated
         # the final multinomial's Exp noise (:171) comes after r; its dtype only changes rounding
         E = noise.exponential((V,)) if proc.stochastic else None
-        step = spec_resample(rows, q, p, n, proc, E, skip_sample_adjustment)
+        step = spec_resample(rows, q, p, n, proc, E, skip_sample_adjustment, exact)
         ids[0, cur + n:cur + g] = pad_token_id                     # :176-177
         ids[0, cur + n] = step.x
         cur += n + 1
@@ -259,7 +284,7 @@ def speculative_generate(inputs: List[int], drafter, target, gamma: int = 5,
 def engine_verify_rows(p_probs: torch.Tensor, q_probs: torch.Tensor, draft_tokens: torch.Tensor,
                        finished: torch.Tensor, end_tokens: Sequence[int], step: int,
                        generated: torch.Tensor, acc_per_seq: torch.Tensor,
-                       noise: TorchNoise) -> List[int]:
+                       noise: TorchNoise, exact: bool = False) -> List[int]:
     """Accept/reject for every active row, ascending, mutating generated/finished/acc_per_seq.
 
     p_probs [B, γ_w, V] (logits dtype), q_probs [B, γ_w, V] fp32.  Returns per-row accepted counts
@@ -288,7 +313,7 @@ def engine_verify_rows(p_probs: torch.Tensor, q_probs: torch.Tensor, draft_token
                     break
             else:
                 res = torch.clamp(p_vec - torch.minimum(p_vec, q_vec), min=0.0)   # :317
-                den = float(res.sum())                             # :318
+                den = float(res.double().sum() if exact else res.sum())   # :318
                 if den <= 1e-12:                                   # :319-321
                     tok_new = int(multinomial(p_vec, noise.exponential(p_vec.shape)).reshape(-1)[0])
                 else:                                              # :323-325
@@ -307,7 +332,7 @@ def engine_verify_rows(p_probs: torch.Tensor, q_probs: torch.Tensor, draft_token
 
 
 def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor,
-                               batch_size: int, noise: Optional[TorchNoise] = None
+                               batch_size: int, noise: Optional[TorchNoise] = None, exact: bool = False
                                ) -> Tuple[List[torch.Tensor], List[float]]:
     """engine/infer_engine.py:149-359 restated on an explicit noise source (CPU)."""
     noise = noise or TorchNoise()
@@ -330,7 +355,7 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
                 break
             prev = (gen[:, step - 1] if step > 0 else input_ids[:, -1]) if d == 0 else gen[:, step + d - 1]
             out = ctx.drafter(prev.unsqueeze(1), past_key_values=past, use_cache=True)
-            qp = torch.softmax(out.logits[:, -1, :], dim=-1)       # :241
+            qp = softmax(out.logits[:, -1, :], exact)              # :241
             past = out.past_key_values
             smp = multinomial(qp, noise.exponential(qp.shape)).squeeze(-1)   # :246
             qfull[:, d, :] = qp                                    # :247
@@ -343,8 +368,8 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
         if bool(act.any()):
             vids = torch.cat([input_ids, gen[:, :step + gw]], dim=1)        # :269-270
             logits = ctx.target(vids).logits[:, -(gw + 1):-1, :]            # :273-275
-            p = torch.softmax(logits, dim=-1)                               # :276
-            engine_verify_rows(p, qfull, drafts, finished, ctx.end_tokens, step, gen, acc, noise)
+            p = softmax(logits, exact)                                      # :276
+            engine_verify_rows(p, qfull, drafts, finished, ctx.end_tokens, step, gen, acc, noise, exact)
         step += gw                                                          # :338
     outs, rates = [], []
     for i in range(B):                                                      # :341-357

@@ -1,0 +1,922 @@
+// specdec_kernels.hip — fused speculative verify/accept/resample for MI355X (gfx950).
+//
+// One verify step (sd_verify) is a short chain of memory-bound kernels on one stream,
+// with no host sync and no allocation:
+//
+//   k_threshold  (top-k / nucleus rows only) radix descent for the keep threshold   -> RowKeep
+//   k_stats      grid (chunk, row): per-chunk max / Σexp of the processed row      -> partials
+//   k_decide     grid (B): combine partials -> (M, S) per row; p(x_i), q(x_i)
+//   k_walk       accept rule walk (A8 / A10), noise offsets, per-row decision
+//   k_resample   grid (chunk, B): Σ(p_n - q_n)+ and exact argmax candidates of the
+//                residual / bonus / p-row sample, in ONE pass over the two rows
+//   k_finalize   grid (B): combine, exact candidate evaluation, outputs, engine state
+//
+// Every logit row is read once by k_stats (the algorithmic bytes); k_resample re-reads
+// at most two rows per sequence (served from the 256 MiB Infinity Cache).  See DESIGN.md.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+
+#include "sd_device.h"
+
+namespace sd {
+
+constexpr int kMaxCand = 8;
+
+struct Decision {
+    int32_t n;          // accepted drafts
+    int32_t mode;       // kModeNone / Bonus / Resid / PRow
+    int32_t slot;       // target slot sampled from (bonus: gamma, resid/prow: n)
+    int32_t status;     // SD_ROW_* bits
+    int64_t noise_off;  // STREAM: word offset of the Exp noise; PHILOX: unused
+    int32_t stop_index;
+    int32_t pad;
+};
+enum { kModeNone = 0, kModeBonus = 1, kModeResid = 2, kModePRow = 3 };
+
+struct ResPart {
+    float sum;                 // Σ residual over the chunk
+    float wmax;                // max residual / E
+    int32_t ncand;             // candidates kept (> kMaxCand => overflow)
+    float pval;                // argmax value (bonus / p-row / engine p fallback)
+    int32_t pidx;
+    float cres[kMaxCand];      // candidate residual value
+    float ce[kMaxCand];        // candidate noise value
+    int32_t cidx[kMaxCand];
+};
+
+struct Plan {
+    int32_t B, gamma, V, rule;
+    int32_t n_tslots, n_dslots, slots, n_chunks, chunk;
+    int32_t tdt, ddt, draft_is_probs, skip_adj;
+    int32_t t_keep, d_keep, t_stoch, n_stop;
+    float tT, dT;
+    const void* trow[SD_MAX_GAMMA + 1];
+    int64_t tstride;
+    const void* drow[SD_MAX_GAMMA];
+    int64_t dstride;
+    const int64_t* draft_tokens;
+    int64_t tok_stride;
+    const int64_t* stops;
+    const uint8_t* active;
+    sd_noise noise;
+    // outputs
+    int32_t* n_accepted;
+    int64_t* next_token;
+    int64_t next_token_stride;
+    float* resample_mass;
+    int32_t* prune_drafter;
+    int32_t* prune_target;
+    int32_t* stop_index;
+    int32_t* row_status;
+    int64_t* words_used;
+    float* token_prob;
+    int64_t* generated;
+    int64_t gen_stride;
+    int32_t step;
+    uint8_t* finished;
+    int64_t* accepted_count;
+    // workspace
+    float2* part;
+    float2* rowstat;
+    RowKeep* keep;
+    float* rp;
+    float* rq;
+    Decision* dec;
+    ResPart* rpart;
+    int32_t* keep_hist;   // threshold scratch
+};
+
+__device__ __forceinline__ const void* row_ptr(const Plan& P, int r, int* dt, float* T, bool* keep) {
+    const int b = r / P.slots, s = r - b * P.slots;
+    if (s < P.n_tslots) {
+        *dt = P.tdt; *T = P.tT; *keep = P.t_keep;
+        return static_cast<const char*>(P.trow[s]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
+    }
+    *dt = P.ddt; *T = P.dT; *keep = P.d_keep;
+    return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
+}
+
+__device__ __forceinline__ bool is_stop(const Plan& P, int64_t tok) {
+    for (int k = 0; k < P.n_stop; ++k)
+        if (P.stops[k] == tok) return true;
+    return false;
+}
+
+// ------------------------------------------------------------------ block helpers
+template <typename F>
+__device__ __forceinline__ float block_reduce(float v, F op, float* lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, kWave));
+    __syncthreads();
+    if (lane == 0) lds[w] = v;
+    __syncthreads();
+    float r = lds[0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = op(r, lds[k]);
+    return r;
+}
+
+__device__ __forceinline__ void block_argmax(float& v, int32_t& i, float* ldsv, int32_t* ldsi) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    wave_argmax(v, i);
+    __syncthreads();
+    if (lane == 0) { ldsv[w] = v; ldsi[w] = i; }
+    __syncthreads();
+    v = ldsv[0]; i = ldsi[0];
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+        if (arg_better(ldsv[k], ldsi[k], v, i)) { v = ldsv[k]; i = ldsi[k]; }
+}
+
+struct FMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
+struct FSum { __device__ float operator()(float a, float b) const { return a + b; } };
+
+// ------------------------------------------------------------------ k_stats
+// Per (chunk, row): max and Σexp of y = round_dt(_process(x)/T) over the chunk.
+template <int DT, int EPT>
+__device__ void stats_body(const Plan& P, const void* row, float T, bool has_keep, int r, int c) {
+    __shared__ float lds[8];
+    constexpr int VEC = Elem<DT>::kVec, NV = EPT / VEC;
+    const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+    const RowKeep kp = has_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const int64_t base = (int64_t)c * P.chunk;
+    float y[EPT];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+        load_vec<DT>(row, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, P.V, aligned, &y[v * VEC]);
+    float m = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int64_t j = base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k;
+            const float t = process_value<DT>(y[v * VEC + k], j, T, has_keep, kp);
+            y[v * VEC + k] = (j < P.V) ? t : -INFINITY;
+            m = fmaxf(m, y[v * VEC + k]);
+        }
+    m = block_reduce(m, FMax(), lds);
+    float s = 0.f;
+    if (m > -INFINITY) {
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) s += expf(y[k] - m);
+    }
+    s = block_reduce(s, FSum(), lds);
+    if (threadIdx.x == 0) P.part[(int64_t)r * P.n_chunks + c] = make_float2(m, s);
+}
+
+template <int EPT>
+__global__ void __launch_bounds__(kThreads) k_stats(Plan P) {
+    const int r = blockIdx.y, c = blockIdx.x;
+    int dt; float T; bool keep;
+    const void* row = row_ptr(P, r, &dt, &T, &keep);
+    if (dt == SD_BF16) stats_body<SD_BF16, EPT>(P, row, T, keep, r, c);
+    else if (dt == SD_F32) stats_body<SD_F32, EPT>(P, row, T, keep, r, c);
+    else stats_body<SD_F16, EPT>(P, row, T, keep, r, c);
+}
+
+// combine the chunk partials of row r (one wave)
+__device__ __forceinline__ float2 combine_row(const Plan& P, int r) {
+    const int lane = threadIdx.x & 63;
+    const float2* pr = P.part + (int64_t)r * P.n_chunks;
+    float m = -INFINITY;
+    for (int c = lane; c < P.n_chunks; c += kWave) m = fmaxf(m, pr[c].x);
+    m = wave_max(m);
+    // fixed-order sum: lane-strided partial sums, then a fixed butterfly
+    float s = 0.f;
+    for (int c = lane; c < P.n_chunks; c += kWave)
+        if (pr[c].x > -INFINITY) s += pr[c].y * expf(pr[c].x - m);
+    s = wave_sum(s);
+    return make_float2(m, s);
+}
+
+template <int DT>
+__device__ __forceinline__ float prob_at(const void* row, int64_t j, float T, bool has_keep, const RowKeep& kp,
+                                         float2 ms) {
+    const float y = process_value<DT>(load_one<DT>(row, j), j, T, has_keep, kp);
+    return round_dt<DT>(expf(y - ms.x) / ms.y);
+}
+
+__device__ __forceinline__ float prob_dyn(int dt, const void* row, int64_t j, float T, bool has_keep,
+                                          const RowKeep& kp, float2 ms) {
+    if (dt == SD_BF16) return prob_at<SD_BF16>(row, j, T, has_keep, kp, ms);
+    if (dt == SD_F32) return prob_at<SD_F32>(row, j, T, has_keep, kp, ms);
+    return prob_at<SD_F16>(row, j, T, has_keep, kp, ms);
+}
+
+// ------------------------------------------------------------------ k_decide
+// grid (B), one wave: row stats for every slot of sequence b, then p(x_i), q(x_i).
+__global__ void __launch_bounds__(64) k_decide(Plan P) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    for (int s = 0; s < P.slots; ++s) {
+        const float2 ms = combine_row(P, b * P.slots + s);
+        if (lane == 0) P.rowstat[b * P.slots + s] = ms;
+    }
+    __syncthreads();
+    if (lane < P.gamma) {
+        const int i = lane;
+        const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
+        int dt; float T; bool keep;
+        const int rt = b * P.slots + i;
+        const void* trow = row_ptr(P, rt, &dt, &T, &keep);
+        const RowKeep kt = keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+        float p = 0.f, q = 0.f;
+        if (tok >= 0 && tok < P.V) {
+            p = prob_dyn(dt, trow, tok, T, keep, kt, P.rowstat[rt]);
+            if (P.draft_is_probs) {
+                q = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
+            } else {
+                const int rd = b * P.slots + P.n_tslots + i;
+                const void* drow = row_ptr(P, rd, &dt, &T, &keep);
+                const RowKeep kd = keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+                q = prob_dyn(dt, drow, tok, T, keep, kd, P.rowstat[rd]);
+            }
+        }
+        P.rp[b * P.gamma + i] = p;
+        P.rq[b * P.gamma + i] = q;
+    }
+}
+
+// ------------------------------------------------------------------ k_walk
+__device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64_t woff, bool* overrun) {
+    if (P.noise.mode == SD_NOISE_STREAM) {
+        if (woff >= P.noise.n_words) { *overrun = true; return 0.f; }
+        return uniform_from_word(P.noise.words[woff]);
+    }
+    return uniform_from_word(philox_block(P.noise, (uint32_t)b, kSiteAccept, (uint32_t)i).x);
+}
+
+// Walk one sequence; returns words consumed (STREAM).  woff = first word of this sequence.
+__device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
+    Decision d{};
+    d.stop_index = -1;
+    d.noise_off = 0;
+    int64_t used = 0;
+    bool overrun = false;
+    const int g = P.gamma;
+    const int64_t sample_words = 2ll * P.V;
+    if (P.rule == SD_RULE_SPEC) {
+        // sampling/speculative_decoding.py:139-145: r = rand(γ'); n = first i with r_i > p_i/q_i
+        int n = g;
+        for (int i = 0; i < g; ++i) {
+            const float r = draw_uniform(P, b, i, woff + i, &overrun);
+            const float frac = P.rp[b * g + i] / P.rq[b * g + i];
+            if (r > frac && n == g) n = i;
+        }
+        used = g;
+        d.n = n;
+        // :150-155 stop token among the accepted drafts -> the reference returns before sampling
+        for (int j = 0; j < n; ++j)
+            if (is_stop(P, P.draft_tokens[b * P.tok_stride + j])) { d.stop_index = j; break; }
+        if (d.stop_index >= 0) {
+            d.mode = kModeNone;
+            d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
+        } else {
+            if (n == g) { d.mode = kModeBonus; d.slot = g; d.status = SD_ROW_DONE | SD_ROW_BONUS; }
+            else if (P.skip_adj) { d.mode = kModePRow; d.slot = n; d.status = SD_ROW_DONE | SD_ROW_FALLBACK_P; }
+            else { d.mode = kModeResid; d.slot = n; d.status = SD_ROW_DONE | SD_ROW_RESIDUAL; }
+            d.noise_off = woff + used;
+            if (P.t_stoch) used += sample_words;
+        }
+        if (P.prune_drafter) P.prune_drafter[b] = (n < g && d.stop_index < 0) ? g - n : 0;
+        if (P.prune_target) P.prune_target[b] = (n < g && d.stop_index < 0) ? g - n + 1 : 0;
+    } else {
+        // engine/infer_engine.py:287-330
+        const bool act = P.active == nullptr || P.active[b] != 0;
+        d.mode = kModeNone;
+        d.n = 0;
+        if (act) {
+            d.status = SD_ROW_DONE;
+            for (int i = 0; i < g; ++i) {
+                const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
+                const double p = P.rp[b * g + i], q = P.rq[b * g + i];
+                const double ap = q <= 0.0 ? 1.0 : fmin(1.0, p / q);
+                const float u = draw_uniform(P, b, i, woff + used, &overrun);
+                used += 1;
+                if ((double)u < ap) {
+                    d.n += 1;
+                    if (is_stop(P, tok)) { d.status |= SD_ROW_FINISHED; break; }
+                } else {
+                    d.mode = kModeResid;
+                    d.slot = i;
+                    d.status |= SD_ROW_RESIDUAL;
+                    d.noise_off = woff + used;
+                    used += sample_words;
+                    break;
+                }
+            }
+        }
+    }
+    if (overrun || (P.noise.mode == SD_NOISE_STREAM && d.mode != kModeNone && P.t_stoch &&
+                    d.noise_off + sample_words > P.noise.n_words))
+        d.status |= SD_ROW_NOISE_OVERRUN;
+    P.dec[b] = d;
+    P.n_accepted[b] = d.n;
+    if (P.stop_index) P.stop_index[b] = d.stop_index;
+    return used;
+}
+
+__global__ void __launch_bounds__(256) k_walk(Plan P) {
+    if (P.noise.mode == SD_NOISE_STREAM) {
+        // the reference draws row after row from one generator: serial by construction
+        if (threadIdx.x == 0) {
+            int64_t off = 0;
+            for (int b = 0; b < P.B; ++b) off += walk_seq(P, b, off);
+            if (P.words_used) *P.words_used = off;
+        }
+    } else {
+        for (int b = threadIdx.x; b < P.B; b += blockDim.x) walk_seq(P, b, 0);
+        if (threadIdx.x == 0 && P.words_used) *P.words_used = 0;
+    }
+}
+
+// ------------------------------------------------------------------ noise per element
+__device__ __forceinline__ float exp_noise(const sd_noise& nz, int64_t woff, int row, int64_t j) {
+    if (nz.mode == SD_NOISE_STREAM) {
+        const int64_t w = woff + 2 * j;
+        if (w + 1 >= nz.n_words) return 1.f;   // overrun is flagged by the walk
+        return exp1_from_words(nz.words[w], nz.words[w + 1]);
+    }
+    const uint4 q = philox_block(nz, (uint32_t)row, kSiteSample, (uint32_t)(j >> 1));
+    return (j & 1) ? exp1_from_words(q.z, q.w) : exp1_from_words(q.x, q.y);
+}
+
+// ------------------------------------------------------------------ k_resample
+// grid (chunk, B).  RESID: residual sum + argmax candidates; BONUS / PROW: argmax of the
+// multinomial (or greedy) value over the processed target row.
+template <int TDT, int DDT, int EPT>
+__device__ void resample_body(const Plan& P, const Decision& d, int b, int c) {
+    __shared__ float ldsf[8];
+    __shared__ int32_t ldsi[8];
+    __shared__ int32_t lcount;
+    __shared__ float lres[kMaxCand], le[kMaxCand];
+    __shared__ int32_t lidx[kMaxCand];
+    constexpr int VEC = Elem<TDT>::kVec < Elem<DDT>::kVec ? Elem<TDT>::kVec : Elem<DDT>::kVec;
+    constexpr int NV = EPT / VEC;
+    const int rt = b * P.slots + d.slot;
+    const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
+    const bool t_al = (reinterpret_cast<uintptr_t>(trow) & 15) == 0;
+    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const float2 mst = P.rowstat[rt];
+    const bool resid = d.mode == kModeResid;
+    const bool stoch = P.t_stoch != 0;
+    const int64_t base = (int64_t)c * P.chunk;
+
+    const void* drow = nullptr;
+    bool d_al = false;
+    RowKeep kd{-INFINITY, INT_MAX, 0, 0};
+    float2 msd = make_float2(0.f, 1.f);
+    if (resid) {
+        if (P.draft_is_probs) {
+            drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
+        } else {
+            const int rd = b * P.slots + P.n_tslots + d.slot;
+            drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
+            if (P.d_keep) kd = P.keep[rd];
+            msd = P.rowstat[rd];
+        }
+        d_al = (reinterpret_cast<uintptr_t>(drow) & 15) == 0;
+    }
+
+    float sum = 0.f, wmax = 0.f;
+    float pv = -INFINITY;      // argmax (value, idx) of the p-based sample
+    int32_t pi = INT_MAX;
+    float res[EPT], ev[EPT];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+        float xt[VEC], xd[VEC];
+        load_vec<TDT>(trow, e0, P.V, t_al, xt);
+        if (resid) {
+            if (P.draft_is_probs) load_vec<SD_F32>(drow, e0, P.V, d_al, xd);
+            else load_vec<DDT>(drow, e0, P.V, d_al, xd);
+        }
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int64_t j = e0 + k;
+            const int idx = v * VEC + k;
+            res[idx] = 0.f;
+            ev[idx] = 1.f;
+            if (j >= P.V) continue;
+            const float p = round_dt<TDT>(expf(process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt) - mst.x) / mst.y);
+            const float e = stoch ? exp_noise(P.noise, d.noise_off, b, j) : 1.f;
+            ev[idx] = e;
+            if (resid) {
+                const float q = P.draft_is_probs
+                    ? xd[k]
+                    : round_dt<DDT>(expf(process_value<DDT>(xd[k], j, P.dT, P.d_keep, kd) - msd.x) / msd.y);
+                const float diff = p - q;                          // bf16/fp32 - fp32 -> fp32
+                const float rr = diff > 0.f ? diff : 0.f;          // max_fn numerator / clamp(p - min(p,q), 0)
+                res[idx] = rr;
+                sum += rr;
+                const float w = rr / e;
+                wmax = fmaxf(wmax, w);
+            }
+            // p-based sample value: bonus / p-row, or the engine's den<=1e-12 fallback
+            const float val = stoch ? round_dt<TDT>(p / round_dt<TDT>(e)) : p;
+            if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
+        }
+    }
+    block_argmax(pv, pi, ldsf, ldsi);
+    float bsum = 0.f, bw = 0.f;
+    if (resid) {
+        bsum = block_reduce(sum, FSum(), ldsf);
+        bw = block_reduce(wmax, FMax(), ldsf);
+        if (threadIdx.x == 0) lcount = 0;
+        __syncthreads();
+        // candidates: any j whose exact value fl(fl(res/S)/E) can equal the max must have
+        // res/E within two fp32 roundings (plus this division's) of the max.
+        const float thr = bw * (1.0f - 4.0f * 5.9604645e-08f);
+        if (bw > 0.f) {
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int idx = v * VEC + k;
+                    const int64_t j = base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k;
+                    if (res[idx] > 0.f && res[idx] / ev[idx] >= thr) {
+                        const int slot = atomicAdd(&lcount, 1);
+                        if (slot < kMaxCand) { lres[slot] = res[idx]; le[slot] = ev[idx]; lidx[slot] = (int32_t)j; }
+                    }
+                }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ResPart& o = P.rpart[(int64_t)b * P.n_chunks + c];
+        o.pval = pv;
+        o.pidx = pi;
+        o.sum = bsum;
+        o.wmax = bw;
+        o.ncand = resid ? lcount : 0;
+        if (resid)
+            for (int k = 0; k < kMaxCand && k < lcount; ++k) { o.cres[k] = lres[k]; o.ce[k] = le[k]; o.cidx[k] = lidx[k]; }
+    }
+}
+
+template <int EPT>
+__global__ void __launch_bounds__(kThreads) k_resample(Plan P) {
+    const int b = blockIdx.y, c = blockIdx.x;
+    const Decision d = P.dec[b];
+    if (d.mode == kModeNone || (d.status & SD_ROW_NOISE_OVERRUN)) return;
+    const int td = P.tdt, dd = P.draft_is_probs ? SD_F32 : P.ddt;
+#define SD_RS(T, D) if (td == T && dd == D) { resample_body<T, D, EPT>(P, d, b, c); return; }
+    SD_RS(SD_BF16, SD_BF16) SD_RS(SD_F32, SD_F32) SD_RS(SD_BF16, SD_F32) SD_RS(SD_F32, SD_BF16)
+    SD_RS(SD_F16, SD_F16) SD_RS(SD_F16, SD_F32) SD_RS(SD_BF16, SD_F16) SD_RS(SD_F16, SD_BF16)
+    SD_RS(SD_F32, SD_F16)
+#undef SD_RS
+}
+
+// ------------------------------------------------------------------ k_finalize
+// grid (B), one wave.
+__global__ void __launch_bounds__(64) k_finalize(Plan P) {
+    const int b = blockIdx.x, lane = threadIdx.x;
+    const Decision d = P.dec[b];
+    const int g = P.gamma;
+    int64_t x = -1;
+    float mass = NAN;
+    int32_t status = d.status;
+    if (d.mode != kModeNone && !(status & SD_ROW_NOISE_OVERRUN)) {
+        const ResPart* rp = P.rpart + (int64_t)b * P.n_chunks;
+        // p-based argmax across chunks (bonus / p-row / engine fallback)
+        float pv = -INFINITY;
+        int32_t pi = INT_MAX;
+        for (int c = lane; c < P.n_chunks; c += kWave)
+            if (arg_better(rp[c].pval, rp[c].pidx, pv, pi)) { pv = rp[c].pval; pi = rp[c].pidx; }
+        wave_argmax(pv, pi);
+        if (d.mode == kModeResid) {
+            // fixed-order residual sum (chunk order is lane-strided, then butterfly)
+            float s = 0.f, wm = 0.f;
+            int overflow = 0;
+            for (int c = lane; c < P.n_chunks; c += kWave) {
+                s += rp[c].sum;
+                wm = fmaxf(wm, rp[c].wmax);
+            }
+            s = wave_sum(s);
+            wm = wave_max(wm);
+            mass = s;
+            const bool engine_fallback = (P.rule == SD_RULE_ENGINE) && ((double)s <= 1e-12);
+            if (engine_fallback) {
+                x = pi;
+                status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
+            } else if (s == 0.f) {
+                // max_fn divides by zero: all-NaN distribution
+                if (P.t_stoch) status |= SD_ROW_INVALID_DIST;
+                else x = 0;   // torch.argmax over an all-NaN row
+            } else {
+                // exact evaluation of the candidates: v = fl(fl(res / S) / E)
+                const float thr = wm * (1.0f - 4.0f * 5.9604645e-08f);
+                float bv = -INFINITY;
+                int32_t bi = INT_MAX;
+                for (int c = lane; c < P.n_chunks; c += kWave) {
+                    const ResPart& o = rp[c];
+                    if (o.wmax < thr) continue;
+                    if (o.ncand > kMaxCand) { overflow = 1; continue; }
+                    for (int k = 0; k < o.ncand; ++k) {
+                        const float pr = o.cres[k] / s;
+                        const float v = P.t_stoch ? pr / o.ce[k] : pr;
+                        if (arg_better(v, o.cidx[k], bv, bi)) { bv = v; bi = o.cidx[k]; }
+                    }
+                }
+                wave_argmax(bv, bi);
+                // overflowing chunks (many near-equal values, e.g. ties) are re-scanned exactly
+                overflow = __any(overflow);
+                if (overflow) {
+                    const int rt = b * P.slots + d.slot;
+                    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+                    const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
+                    const float2 mst = P.rowstat[rt];
+                    const void* drow;
+                    RowKeep kd{-INFINITY, INT_MAX, 0, 0};
+                    float2 msd = make_float2(0.f, 1.f);
+                    int ddt = SD_F32;
+                    if (P.draft_is_probs) drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
+                    else {
+                        const int rd = b * P.slots + P.n_tslots + d.slot;
+                        drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
+                        if (P.d_keep) kd = P.keep[rd];
+                        msd = P.rowstat[rd];
+                        ddt = P.ddt;
+                    }
+                    for (int64_t j = lane; j < P.V; j += kWave) {
+                        const float p = prob_dyn(P.tdt, trow, j, P.tT, P.t_keep, kt, mst);
+                        const float q = P.draft_is_probs ? static_cast<const float*>(drow)[j]
+                                                         : prob_dyn(ddt, drow, j, P.dT, P.d_keep, kd, msd);
+                        const float diff = p - q;
+                        const float rr = diff > 0.f ? diff : 0.f;
+                        const float pr = rr / s;
+                        const float v = P.t_stoch ? pr / exp_noise(P.noise, d.noise_off, b, j) : pr;
+                        if (arg_better(v, (int32_t)j, bv, bi)) { bv = v; bi = (int32_t)j; }
+                    }
+                    wave_argmax(bv, bi);
+                }
+                x = bi;
+            }
+        } else {
+            x = pi;
+        }
+    }
+    if (lane == 0) {
+        P.next_token[b * P.next_token_stride] = x;
+        if (P.resample_mass) P.resample_mass[b] = mass;
+        // engine/infer_engine.py:307-336 applied in place
+        const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
+        if (engine_state && (status & SD_ROW_DONE)) {
+            int64_t* gen = P.generated + b * P.gen_stride;
+            if (d.mode == kModeResid && x >= 0) {
+                gen[P.step + d.n] = x;
+                if (is_stop(P, x)) status |= SD_ROW_FINISHED;
+            }
+            if (d.n < g)
+                for (int t = P.step + d.n + 1; t < P.step + g; ++t) gen[t] = 0;
+            if (status & SD_ROW_FINISHED) P.finished[b] = 1;
+            P.accepted_count[b] += d.n;
+        } else if (P.rule == SD_RULE_ENGINE && d.mode == kModeResid && x >= 0 && is_stop(P, x)) {
+            status |= SD_ROW_FINISHED;
+        }
+        if (P.t_keep)
+            for (int s2 = 0; s2 < P.n_tslots; ++s2) status |= P.keep[b * P.slots + s2].flags;
+        if (P.d_keep)
+            for (int s2 = P.n_tslots; s2 < P.slots; ++s2) status |= P.keep[b * P.slots + s2].flags;
+        P.row_status[b] = status;
+    }
+}
+
+// ------------------------------------------------------------------ sd_sample kernels
+// grid (chunk, R): argmax of round_dt(p / round_dt(E)) (multinomial) or p (greedy).
+template <int DT, int EPT>
+__device__ void rowsample_body(const Plan& P, int r, int c) {
+    __shared__ float ldsf[8];
+    __shared__ int32_t ldsi[8];
+    __shared__ float2 lms;
+    constexpr int VEC = Elem<DT>::kVec, NV = EPT / VEC;
+    if (threadIdx.x < 64) {
+        const float2 ms = combine_row(P, r);
+        if (threadIdx.x == 0) lms = ms;
+    }
+    __syncthreads();
+    const float2 ms = lms;
+    const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
+    const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+    const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const int64_t base = (int64_t)c * P.chunk;
+    const int64_t woff = 2ll * P.V * r;
+    float pv = -INFINITY;
+    int32_t pi = INT_MAX;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+        float x[VEC];
+        load_vec<DT>(row, e0, P.V, al, x);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int64_t j = e0 + k;
+            if (j >= P.V) continue;
+            const float p = round_dt<DT>(expf(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
+            const float val = P.t_stoch ? round_dt<DT>(p / round_dt<DT>(exp_noise(P.noise, woff, r, j))) : p;
+            if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
+        }
+    }
+    block_argmax(pv, pi, ldsf, ldsi);
+    if (threadIdx.x == 0) {
+        ResPart& o = P.rpart[(int64_t)r * P.n_chunks + c];
+        o.pval = pv;
+        o.pidx = pi;
+    }
+}
+
+template <int EPT>
+__global__ void __launch_bounds__(kThreads) k_rowsample(Plan P) {
+    const int r = blockIdx.y, c = blockIdx.x;
+    if (P.tdt == SD_BF16) rowsample_body<SD_BF16, EPT>(P, r, c);
+    else if (P.tdt == SD_F32) rowsample_body<SD_F32, EPT>(P, r, c);
+    else rowsample_body<SD_F16, EPT>(P, r, c);
+}
+
+__global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
+    const int r = blockIdx.x, lane = threadIdx.x;
+    const ResPart* rp = P.rpart + (int64_t)r * P.n_chunks;
+    float pv = -INFINITY;
+    int32_t pi = INT_MAX;
+    for (int c = lane; c < P.n_chunks; c += kWave)
+        if (arg_better(rp[c].pval, rp[c].pidx, pv, pi)) { pv = rp[c].pval; pi = rp[c].pidx; }
+    wave_argmax(pv, pi);
+    const float2 ms = combine_row(P, r);
+    if (lane == 0) {
+        int32_t st = SD_ROW_DONE;
+        if (P.t_stoch && (!(ms.y > 0.f) || ms.y != ms.y)) st |= SD_ROW_INVALID_DIST;
+        if (P.t_keep) st |= P.keep[r].flags;
+        if (P.noise.mode == SD_NOISE_STREAM && P.t_stoch && 2ll * P.V * P.B > P.noise.n_words)
+            st |= SD_ROW_NOISE_OVERRUN;
+        P.next_token[r * P.next_token_stride] = pi;
+        if (P.token_prob) {
+            const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
+            const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+            P.token_prob[r] = (pi >= 0 && pi < P.V) ? prob_dyn(P.tdt, row, pi, P.tT, P.t_keep, kp, ms) : NAN;
+        }
+        if (P.row_status) P.row_status[r] = st;
+        if (r == 0 && P.words_used) *P.words_used = P.t_stoch ? 2ll * P.V * P.B : 0;
+    }
+}
+
+// ------------------------------------------------------------------ sd_probs kernel
+template <int DT, int EPT>
+__device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r, int c) {
+    __shared__ float2 lms;
+    constexpr int VEC = Elem<DT>::kVec, NV = EPT / VEC;
+    if (threadIdx.x < 64) {
+        const float2 ms = combine_row(P, r);
+        if (threadIdx.x == 0) lms = ms;
+    }
+    __syncthreads();
+    const float2 ms = lms;
+    const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
+    const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+    const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const int64_t base = (int64_t)c * P.chunk;
+    char* orow = static_cast<char*>(out) + r * ostride * (DT == SD_F32 ? 4 : 2);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+        float x[VEC];
+        load_vec<DT>(row, e0, P.V, al, x);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int64_t j = e0 + k;
+            if (j >= P.V) continue;
+            const float p = round_dt<DT>(expf(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
+            if constexpr (DT == SD_F32) reinterpret_cast<float*>(orow)[j] = p;
+            else if constexpr (DT == SD_BF16) reinterpret_cast<uint16_t*>(orow)[j] = (uint16_t)(__float_as_uint(p) >> 16);
+            else reinterpret_cast<__half*>(orow)[j] = __float2half_rn(p);
+        }
+    }
+}
+
+template <int EPT>
+__global__ void __launch_bounds__(kThreads) k_writeprobs(Plan P, void* out, int64_t ostride) {
+    const int r = blockIdx.y, c = blockIdx.x;
+    if (P.tdt == SD_BF16) writeprobs_body<SD_BF16, EPT>(P, out, ostride, r, c);
+    else if (P.tdt == SD_F32) writeprobs_body<SD_F32, EPT>(P, out, ostride, r, c);
+    else writeprobs_body<SD_F16, EPT>(P, out, ostride, r, c);
+}
+
+}  // namespace sd
+
+// ====================================================================== host side
+#include "sd_threshold.inc"
+
+namespace {
+
+using namespace sd;
+
+constexpr int kEptSmall = 8, kEptLarge = 32;
+
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+struct Carve {
+    char* p;
+    size_t used = 0;
+    template <typename T>
+    T* take(size_t n) {
+        T* r = reinterpret_cast<T*>(p ? p + used : nullptr);
+        used += align256(n * sizeof(T));
+        return r;
+    }
+};
+
+int max_chunks(int vocab) { return (vocab + kThreads * kEptSmall - 1) / (kThreads * kEptSmall); }
+
+void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
+    const int nc = max_chunks(vocab);
+    P.part = c.take<float2>((size_t)rows_total * nc);
+    P.rowstat = c.take<float2>(rows_total);
+    P.keep = c.take<RowKeep>(rows_total);
+    P.rp = c.take<float>((size_t)B * gamma);
+    P.rq = c.take<float>((size_t)B * gamma);
+    P.dec = c.take<Decision>(B);
+    P.rpart = c.take<ResPart>((size_t)(B > rows_total ? B : rows_total) * nc);
+    P.keep_hist = c.take<int32_t>((size_t)rows_total * kThreshScratchInts);
+}
+
+bool valid_dtype(int dt) { return dt == SD_F32 || dt == SD_BF16 || dt == SD_F16; }
+bool valid_proc(const sd_processor& p) {
+    if (p.kind < SD_PROC_GREEDY || p.kind > SD_PROC_TOPK_NUCLEUS) return false;
+    if ((p.kind == SD_PROC_TOPK || p.kind == SD_PROC_TOPK_NUCLEUS) && p.top_k <= 0) return false;
+    return true;
+}
+bool needs_keep(const sd_processor& p) { return p.kind >= SD_PROC_TOPK; }
+
+int choose_ept(int rows, int vocab) {
+    const int64_t big = (int64_t)rows * ((vocab + kThreads * kEptLarge - 1) / (kThreads * kEptLarge));
+    return big >= 2048 ? kEptLarge : kEptSmall;
+}
+
+#define SD_LAUNCH(kern, grid, block, stream, ...)                                             \
+    do {                                                                                      \
+        hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, __VA_ARGS__);            \
+        if (hipGetLastError() != hipSuccess) return SD_ERR_LAUNCH;                            \
+    } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int32_t sd_abi_version(void) { return SD_ABI_VERSION; }
+
+const char* sd_status_string(int32_t s) {
+    switch (s) {
+        case SD_OK: return "ok";
+        case SD_ERR_INVALID: return "invalid argument";
+        case SD_ERR_WORKSPACE: return "workspace too small";
+        case SD_ERR_LAUNCH: return "kernel launch failed";
+        case SD_ERR_UNSUPPORTED: return "unsupported combination";
+        default: return "unknown status";
+    }
+}
+
+size_t sd_verify_workspace_size(int32_t batch, int32_t gamma, int32_t vocab) {
+    if (batch <= 0 || gamma <= 0 || gamma > SD_MAX_GAMMA || vocab <= 0) return 0;
+    Plan P{};
+    Carve c{nullptr};
+    carve(P, c, batch * (2 * gamma + 1), batch, gamma, vocab);
+    return c.used;
+}
+
+int32_t sd_verify(const sd_verify_args* a, void* stream) {
+    if (!a || a->batch <= 0 || a->gamma <= 0 || a->gamma > SD_MAX_GAMMA || a->vocab <= 0) return SD_ERR_INVALID;
+    if (a->rule != SD_RULE_SPEC && a->rule != SD_RULE_ENGINE) return SD_ERR_INVALID;
+    if (!valid_dtype(a->target_dtype) || (!a->draft_is_probs && !valid_dtype(a->draft_dtype))) return SD_ERR_INVALID;
+    if (!valid_proc(a->target_proc) || !valid_proc(a->draft_proc)) return SD_ERR_INVALID;
+    if (!a->draft_tokens || !a->n_accepted || !a->next_token || !a->row_status) return SD_ERR_INVALID;
+    if (a->n_stop > 0 && !a->stop_tokens) return SD_ERR_INVALID;
+    if (a->noise.mode == SD_NOISE_STREAM && !a->noise.words && a->noise.n_words > 0) return SD_ERR_INVALID;
+    if (a->rule == SD_RULE_ENGINE && a->generated && (!a->finished || !a->accepted_count)) return SD_ERR_INVALID;
+    const int n_t = a->rule == SD_RULE_SPEC ? a->gamma + 1 : a->gamma;
+    for (int t = 0; t < n_t; ++t)
+        if (!a->target_rows[t]) return SD_ERR_INVALID;
+    for (int t = 0; t < a->gamma; ++t)
+        if (!a->draft_rows[t]) return SD_ERR_INVALID;
+    if (a->workspace_bytes < sd_verify_workspace_size(a->batch, a->gamma, a->vocab) || !a->workspace)
+        return SD_ERR_WORKSPACE;
+
+    Plan P{};
+    P.B = a->batch; P.gamma = a->gamma; P.V = a->vocab; P.rule = a->rule;
+    P.n_tslots = n_t;
+    P.n_dslots = a->draft_is_probs ? 0 : a->gamma;
+    P.slots = P.n_tslots + P.n_dslots;
+    P.tdt = a->target_dtype; P.ddt = a->draft_is_probs ? SD_F32 : a->draft_dtype;
+    P.draft_is_probs = a->draft_is_probs; P.skip_adj = a->skip_sample_adjustment;
+    P.t_keep = needs_keep(a->target_proc); P.d_keep = !a->draft_is_probs && needs_keep(a->draft_proc);
+    P.t_stoch = a->rule == SD_RULE_ENGINE ? 1 : (a->target_proc.kind != SD_PROC_GREEDY);
+    P.tT = a->target_proc.temperature; P.dT = a->draft_proc.temperature;
+    if (!(P.tT > 0.f) || (!a->draft_is_probs && !(P.dT > 0.f))) return SD_ERR_INVALID;
+    for (int t = 0; t < n_t; ++t) P.trow[t] = a->target_rows[t];
+    P.tstride = a->target_stride_b;
+    for (int t = 0; t < a->gamma; ++t) P.drow[t] = a->draft_rows[t];
+    P.dstride = a->draft_stride_b;
+    P.draft_tokens = a->draft_tokens; P.tok_stride = a->draft_tokens_stride_b;
+    P.stops = a->stop_tokens; P.n_stop = a->n_stop;
+    P.active = a->active; P.noise = a->noise;
+    P.n_accepted = a->n_accepted; P.next_token = a->next_token; P.next_token_stride = 1;
+    P.resample_mass = a->resample_mass; P.prune_drafter = a->prune_drafter; P.prune_target = a->prune_target;
+    P.stop_index = a->stop_index; P.row_status = a->row_status; P.words_used = a->words_used;
+    P.generated = a->generated; P.gen_stride = a->generated_stride_b; P.step = a->step;
+    P.finished = a->finished; P.accepted_count = a->accepted_count;
+
+    const int rows = P.B * P.slots;
+    const int ept = choose_ept(rows, P.V);
+    P.chunk = kThreads * ept;
+    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    Carve c{static_cast<char*>(a->workspace)};
+    carve(P, c, a->batch * (2 * a->gamma + 1), a->batch, a->gamma, a->vocab);
+
+    if (P.t_keep || P.d_keep) {
+        const int32_t st = launch_threshold(P, a->target_proc, a->draft_proc, stream);
+        if (st != SD_OK) return st;
+    }
+    if (ept == kEptLarge) SD_LAUNCH(k_stats<kEptLarge>, dim3(P.n_chunks, rows), dim3(kThreads), stream, P);
+    else SD_LAUNCH(k_stats<kEptSmall>, dim3(P.n_chunks, rows), dim3(kThreads), stream, P);
+    SD_LAUNCH(k_decide, dim3(P.B), dim3(64), stream, P);
+    SD_LAUNCH(k_walk, dim3(1), dim3(256), stream, P);
+    if (ept == kEptLarge) SD_LAUNCH(k_resample<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+    else SD_LAUNCH(k_resample<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+    SD_LAUNCH(k_finalize, dim3(P.B), dim3(64), stream, P);
+    return SD_OK;
+}
+
+size_t sd_sample_workspace_size(int32_t rows, int32_t vocab) {
+    if (rows <= 0 || vocab <= 0) return 0;
+    Plan P{};
+    Carve c{nullptr};
+    carve(P, c, rows, rows, 1, vocab);
+    return c.used;
+}
+
+int32_t sd_sample(const sd_sample_args* a, void* stream) {
+    if (!a || a->rows <= 0 || a->vocab <= 0 || !a->logits || !a->tokens) return SD_ERR_INVALID;
+    if (!valid_dtype(a->dtype) || !valid_proc(a->proc) || !(a->proc.temperature > 0.f)) return SD_ERR_INVALID;
+    if (a->noise.mode == SD_NOISE_STREAM && a->proc.kind != SD_PROC_GREEDY && !a->noise.words) return SD_ERR_INVALID;
+    if (a->workspace_bytes < sd_sample_workspace_size(a->rows, a->vocab) || !a->workspace) return SD_ERR_WORKSPACE;
+    Plan P{};
+    P.B = a->rows; P.gamma = 1; P.V = a->vocab; P.rule = -1;
+    P.n_tslots = 1; P.n_dslots = 0; P.slots = 1;
+    P.tdt = a->dtype; P.ddt = a->dtype;
+    P.t_keep = needs_keep(a->proc); P.t_stoch = a->proc.kind != SD_PROC_GREEDY;
+    P.tT = a->proc.temperature; P.dT = 1.f;
+    P.trow[0] = a->logits; P.tstride = a->stride_r;
+    P.noise = a->noise;
+    P.next_token = a->tokens; P.next_token_stride = a->tokens_stride;
+    P.token_prob = a->token_prob; P.row_status = a->row_status; P.words_used = a->words_used;
+    const int ept = choose_ept(P.B, P.V);
+    P.chunk = kThreads * ept;
+    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    Carve c{static_cast<char*>(a->workspace)};
+    carve(P, c, a->rows, a->rows, 1, a->vocab);
+    if (P.t_keep) {
+        const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
+        if (st != SD_OK) return st;
+    }
+    if (ept == kEptLarge) {
+        SD_LAUNCH(k_stats<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+        SD_LAUNCH(k_rowsample<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+    } else {
+        SD_LAUNCH(k_stats<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+        SD_LAUNCH(k_rowsample<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+    }
+    SD_LAUNCH(k_sample_finalize, dim3(P.B), dim3(64), stream, P);
+    return SD_OK;
+}
+
+size_t sd_probs_workspace_size(int32_t rows, int32_t vocab) { return sd_sample_workspace_size(rows, vocab); }
+
+int32_t sd_probs(const sd_probs_args* a, void* stream) {
+    if (!a || a->rows <= 0 || a->vocab <= 0 || !a->logits || !a->probs) return SD_ERR_INVALID;
+    if (!valid_dtype(a->dtype) || !valid_proc(a->proc) || !(a->proc.temperature > 0.f)) return SD_ERR_INVALID;
+    if (a->workspace_bytes < sd_probs_workspace_size(a->rows, a->vocab) || !a->workspace) return SD_ERR_WORKSPACE;
+    Plan P{};
+    P.B = a->rows; P.gamma = 1; P.V = a->vocab; P.rule = -1;
+    P.n_tslots = 1; P.n_dslots = 0; P.slots = 1;
+    P.tdt = a->dtype; P.ddt = a->dtype;
+    P.t_keep = needs_keep(a->proc);
+    P.tT = a->proc.temperature; P.dT = 1.f;
+    P.trow[0] = a->logits; P.tstride = a->stride_r;
+    const int ept = choose_ept(P.B, P.V);
+    P.chunk = kThreads * ept;
+    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    Carve c{static_cast<char*>(a->workspace)};
+    carve(P, c, a->rows, a->rows, 1, a->vocab);
+    if (P.t_keep) {
+        const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
+        if (st != SD_OK) return st;
+    }
+    if (ept == kEptLarge) {
+        SD_LAUNCH(k_stats<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+        SD_LAUNCH(k_writeprobs<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    } else {
+        SD_LAUNCH(k_stats<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+        SD_LAUNCH(k_writeprobs<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    }
+    return SD_OK;
+}
+
+}  // extern "C"

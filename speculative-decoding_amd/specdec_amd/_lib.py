@@ -1,0 +1,127 @@
+"""ctypes binding of libspecdec.so (include/specdec.h).
+
+The library is built in-tree (``make -C speculative-decoding_amd``) and loaded from this
+package directory.  There is no fallback: if the library is missing or was built for a
+different ABI, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+SD_ABI_VERSION = 1
+SD_MAX_GAMMA = 16
+
+SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
+SD_F32, SD_BF16, SD_F16 = 0, 1, 2
+SD_PROC_GREEDY, SD_PROC_MULTINOMIAL, SD_PROC_TOPK, SD_PROC_NUCLEUS, SD_PROC_TOPK_NUCLEUS = range(5)
+SD_RULE_SPEC, SD_RULE_ENGINE = 0, 1
+SD_NOISE_STREAM, SD_NOISE_PHILOX = 0, 1
+
+SD_ROW_DONE = 0x1
+SD_ROW_STOP_IN_DRAFTS = 0x2
+SD_ROW_FINISHED = 0x4
+SD_ROW_RESIDUAL = 0x8
+SD_ROW_BONUS = 0x10
+SD_ROW_FALLBACK_P = 0x20
+SD_ROW_INVALID_DIST = 0x40
+SD_ROW_NOISE_OVERRUN = 0x80
+SD_ROW_NUCLEUS_INEXACT = 0x100
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspecdec.so")
+
+EXPORTS = ("sd_abi_version", "sd_status_string", "sd_verify_workspace_size", "sd_verify",
+           "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",
+           "sd_mt19937_fill", "sd_mt19937_advance")
+
+
+class sd_processor(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("temperature", C.c_float), ("top_k", C.c_int32), ("top_p", C.c_float)]
+
+
+class sd_noise(C.Structure):
+    _fields_ = [("mode", C.c_int32), ("words", C.c_void_p), ("n_words", C.c_int64),
+                ("seed", C.c_uint64), ("offset", C.c_uint64)]
+
+
+class sd_verify_args(C.Structure):
+    _fields_ = [
+        ("batch", C.c_int32), ("gamma", C.c_int32), ("vocab", C.c_int32), ("rule", C.c_int32),
+        ("target_rows", C.c_void_p * (SD_MAX_GAMMA + 1)), ("target_stride_b", C.c_int64),
+        ("target_dtype", C.c_int32),
+        ("draft_rows", C.c_void_p * SD_MAX_GAMMA), ("draft_stride_b", C.c_int64),
+        ("draft_dtype", C.c_int32), ("draft_is_probs", C.c_int32),
+        ("draft_tokens", C.c_void_p), ("draft_tokens_stride_b", C.c_int64),
+        ("target_proc", sd_processor), ("draft_proc", sd_processor),
+        ("skip_sample_adjustment", C.c_int32), ("stop_tokens", C.c_void_p), ("n_stop", C.c_int32),
+        ("active", C.c_void_p),
+        ("noise", sd_noise),
+        ("n_accepted", C.c_void_p), ("next_token", C.c_void_p), ("resample_mass", C.c_void_p),
+        ("prune_drafter", C.c_void_p), ("prune_target", C.c_void_p), ("stop_index", C.c_void_p),
+        ("row_status", C.c_void_p), ("words_used", C.c_void_p),
+        ("generated", C.c_void_p), ("generated_stride_b", C.c_int64), ("step", C.c_int32),
+        ("finished", C.c_void_p), ("accepted_count", C.c_void_p),
+        ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+    ]
+
+
+class sd_sample_args(C.Structure):
+    _fields_ = [
+        ("rows", C.c_int32), ("vocab", C.c_int32), ("logits", C.c_void_p), ("stride_r", C.c_int64),
+        ("dtype", C.c_int32), ("proc", sd_processor), ("noise", sd_noise),
+        ("tokens", C.c_void_p), ("tokens_stride", C.c_int64), ("token_prob", C.c_void_p),
+        ("row_status", C.c_void_p), ("words_used", C.c_void_p),
+        ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+    ]
+
+
+class sd_probs_args(C.Structure):
+    _fields_ = [
+        ("rows", C.c_int32), ("vocab", C.c_int32), ("logits", C.c_void_p), ("stride_r", C.c_int64),
+        ("dtype", C.c_int32), ("proc", sd_processor), ("probs", C.c_void_p), ("probs_stride_r", C.c_int64),
+        ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+    ]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"specdec_amd: {LIB_PATH} not found — build it with "
+                          f"`make -C speculative-decoding_amd` (hipcc, gfx950)")
+    lib = C.CDLL(LIB_PATH)
+    for name in EXPORTS:
+        if not hasattr(lib, name):
+            raise ImportError(f"specdec_amd: {LIB_PATH} does not export {name}")
+    lib.sd_abi_version.restype = C.c_int32
+    lib.sd_status_string.restype = C.c_char_p
+    lib.sd_status_string.argtypes = [C.c_int32]
+    for ws in ("sd_verify_workspace_size",):
+        getattr(lib, ws).restype = C.c_size_t
+        getattr(lib, ws).argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    for ws in ("sd_sample_workspace_size", "sd_probs_workspace_size"):
+        getattr(lib, ws).restype = C.c_size_t
+        getattr(lib, ws).argtypes = [C.c_int32, C.c_int32]
+    lib.sd_verify.restype = C.c_int32
+    lib.sd_verify.argtypes = [C.POINTER(sd_verify_args), C.c_void_p]
+    lib.sd_sample.restype = C.c_int32
+    lib.sd_sample.argtypes = [C.POINTER(sd_sample_args), C.c_void_p]
+    lib.sd_probs.restype = C.c_int32
+    lib.sd_probs.argtypes = [C.POINTER(sd_probs_args), C.c_void_p]
+    lib.sd_mt19937_fill.restype = C.c_int32
+    lib.sd_mt19937_fill.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64]
+    lib.sd_mt19937_advance.restype = C.c_int32
+    lib.sd_mt19937_advance.argtypes = [C.c_void_p, C.c_size_t, C.c_int64]
+    if lib.sd_abi_version() != SD_ABI_VERSION:
+        raise ImportError(f"specdec_amd: ABI mismatch ({lib.sd_abi_version()} != {SD_ABI_VERSION})")
+    return lib
+
+
+lib = _load()
+
+
+class SpecdecError(RuntimeError):
+    pass
+
+
+def check(status: int, what: str):
+    if status != SD_OK:
+        raise SpecdecError(f"{what}: {lib.sd_status_string(status).decode()} ({status})")

@@ -1,0 +1,155 @@
+"""Batched speculative decoding on the fused HIP path.
+
+Drop-in for engine/infer_engine.py:10-359 (``infer_batch`` -> ``run_batch_speculative`` ->
+``batch_speculative_generate``), same signatures and return values, same bookkeeping.
+
+Per window the drafter runs γ_w single-token forwards with its KV cache; each ``[B, V]``
+drafter row is softmax-sampled by ``sd_sample`` (T=1, :241-246).  The target runs once on the
+whole sequence (no cache, as the reference, :270-276).  ONE ``sd_verify`` call (rule ENGINE)
+then replaces the per-row / per-draft Python loop with its ``.item()`` syncs (:279-336): the
+fp64 ``u < min(1, p/q)`` test, the eos stop, the (p-q)+ residual resample (or the p fallback
+when Σ <= 1e-12) and the in-place updates of ``generated`` / ``finished`` / accepted counts —
+all on the device.  The host syncs once per window (``finished.all()``, :212).
+
+Reference quirks reproduced: no bonus token; zero "gaps" after a
+reject; trailing zeros stripped; padding counted as generated tokens; the drafter cache is
+never pruned.  Not reproduced: the bf16 B>=2 crash at :254 (there is nothing to crash on).
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional, Tuple
+
+import torch
+
+from .. import _lib
+from ..noise import default_noise
+from ..ops import PLAIN_SOFTMAX, sample_rows, verify
+from .batch_decode import decode_batch_with_chat_template
+from .metrics import BatchMetrics, RequestMetrics
+
+
+def infer_batch(ctx, prompts: List[str]) -> Tuple[Optional[BatchMetrics], Optional[BatchMetrics]]:
+    """engine/infer_engine.py:10-96: format, tokenize, dispatch."""
+    if ctx.chat:
+        formatted = [ctx.tokenizer.apply_chat_template([{"role": "user", "content": p}],
+                                                       add_generation_prompt=True, tokenize=False)
+                     for p in prompts]
+    else:
+        formatted = prompts
+    input_ids, attention_mask = decode_batch_with_chat_template(ctx.tokenizer, formatted,
+                                                                max_length=ctx.max_batch_length, chat=False)
+    drafter_device = getattr(ctx, "drafter_device", None)
+    if ctx.spec and drafter_device is not None:
+        input_ids, attention_mask = input_ids.to(drafter_device), attention_mask.to(drafter_device)
+    if getattr(ctx, "reset_in_between", False) and getattr(ctx, "ngram", None) is not None:
+        ctx.ngram.reset()
+    if ctx.spec:
+        return run_batch_speculative(ctx, input_ids, attention_mask, len(prompts)), None
+    if getattr(ctx, "target_gen", False):
+        raise NotImplementedError("target-only autoregressive decoding is outside the verify/accept path")
+    return None, None
+
+
+def run_batch_speculative(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor,
+                          batch_size: int) -> Optional[BatchMetrics]:
+    """engine/infer_engine.py:99-146: run the batch and fill BatchMetrics (same rules)."""
+    bm = BatchMetrics(batch_size=batch_size)
+    bm.batch_start_time = time.time()
+    starts = [time.time()] * batch_size
+    firsts: List[Optional[float]] = [None] * batch_size
+
+    def first_token(idx):
+        if idx < batch_size and firsts[idx] is None:
+            firsts[idx] = time.time()
+
+    try:
+        outputs, rates = batch_speculative_generate(ctx, input_ids, attention_mask, batch_size,
+                                                    first_token_callback=first_token)
+    except Exception as e:  # the reference's contract: report and return None (:144-146)
+        print(f"Batch speculative decoding failed: {type(e).__name__}: {e}")
+        return None
+    bm.batch_end_time = time.time()
+    prompt_tokens = attention_mask.sum(dim=1).tolist()
+    for i in range(batch_size):
+        r = RequestMetrics()
+        r.start_time = starts[i]
+        r.prompt_tokens = int(prompt_tokens[i])
+        r.generated_tokens = len(outputs[i]) - r.prompt_tokens
+        r.total_tokens = len(outputs[i])
+        r.acceptance_rate = rates[i] if i < len(rates) else 0.0
+        r.end_time = bm.batch_end_time
+        if firsts[i] is not None:
+            r.first_token_time = firsts[i]
+            r.ttft = firsts[i] - starts[i]
+        else:
+            r.ttft = (bm.batch_end_time - starts[i]) / max(r.generated_tokens, 1)
+        r.total_latency = bm.batch_end_time - starts[i]
+        bm.requests.append(r)
+    return bm
+
+
+@torch.no_grad()
+def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor, batch_size: int,
+                               first_token_callback=None) -> Tuple[List[torch.Tensor], List[float]]:
+    """engine/infer_engine.py:149-359 with the accept loop fused into sd_verify."""
+    dev = input_ids.device
+    if dev.type != "cuda":
+        raise RuntimeError("specdec_amd.batch_speculative_generate runs on the GPU (HIP); input_ids are on "
+                           f"{dev}. There is no CPU path.")
+    target_device = getattr(ctx, "target_device", dev)
+    B = batch_size
+    gen_len, gamma = int(ctx.gen_len), int(ctx.gamma)
+    noise = default_noise()
+    generated = torch.zeros(B, gen_len, dtype=torch.long, device=dev)
+    finished = torch.zeros(B, dtype=torch.uint8, device=dev)
+    drafted = torch.zeros(B, dtype=torch.long, device=dev)
+    accepted = torch.zeros(B, dtype=torch.long, device=dev)
+    stops = torch.tensor(list(ctx.end_tokens), dtype=torch.long, device=dev)
+
+    past = ctx.drafter(input_ids, attention_mask=attention_mask, use_cache=True).past_key_values   # :206
+    step = 0
+    while step < gen_len:                                                 # :211
+        if bool(finished.all()):
+            break
+        gw = min(gamma, gen_len - step)                                   # :216
+        draft_tokens = torch.zeros(B, gw, dtype=torch.long, device=dev)
+        active = finished == 0
+        rows = []
+        for d in range(gw):                                               # :224 (finished is constant here)
+            if d == 0:
+                prev = generated[:, step - 1] if step > 0 else input_ids[:, -1]
+            else:
+                prev = generated[:, step + d - 1]
+            out = ctx.drafter(prev.unsqueeze(1), past_key_values=past, use_cache=True)   # :239
+            logits = out.logits[:, -1, :]
+            past = out.past_key_values
+            samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise)     # :241-246 softmax + multinomial
+            rows.append(logits)
+            draft_tokens[:, d] = torch.where(active, samples, draft_tokens[:, d])          # :252
+            generated[:, step + d] = torch.where(active, samples, generated[:, step + d])  # :257
+            drafted += active.long()                                      # :258
+            if first_token_callback is not None and d == 0 and step == 0:
+                for idx in torch.nonzero(active).flatten().tolist():
+                    first_token_callback(idx)
+        verify_ids = torch.cat([input_ids, generated[:, :step + gw]], dim=1).to(target_device)  # :269-270
+        t_logits = ctx.target(verify_ids).logits                          # :273
+        L = t_logits.shape[1]
+        trows = [t_logits[:, L - gw - 1 + t, :] for t in range(gw)]      # :275 logits[:, -(γ+1):-1]
+        if any(r.device != t_logits.device for r in rows):
+            rows = [r.to(t_logits.device) for r in rows]
+        verify(trows, rows, draft_tokens, _lib.SD_RULE_ENGINE, PLAIN_SOFTMAX, PLAIN_SOFTMAX, noise, stops,
+               active=active.to(torch.uint8),
+               engine_state=dict(generated=generated, step=step, finished=finished, accepted=accepted))
+        step += gw                                                        # :338
+
+    gen_host = generated.cpu()
+    drafted_h, accepted_h = drafted.tolist(), accepted.tolist()
+    outputs, rates = [], []
+    for i in range(B):                                                    # :341-357
+        nz = torch.nonzero(gen_host[i], as_tuple=True)[0]
+        tail = gen_host[i, :int(nz[-1]) + 1] if nz.numel() > 0 else torch.empty(0, dtype=torch.long)
+        outputs.append(torch.cat([input_ids[i], tail.to(dev)]))
+        t, a = drafted_h[i], accepted_h[i]
+        rates.append(a / t if t > 0 else 0.0)
+    return outputs, rates

@@ -1,0 +1,250 @@
+"""Tensor-level wrappers over the C ABI (include/specdec.h).
+
+Every call validates shapes, strides and dtypes on the host BEFORE a kernel is enqueued,
+then launches on the current HIP stream of the tensors' device.  Nothing here syncs except
+where noted (StreamNoise needs the consumed word count to advance the torch generator).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import lib
+from .noise import PhiloxNoise, StreamNoise
+
+_DT = {torch.float32: _lib.SD_F32, torch.bfloat16: _lib.SD_BF16, torch.float16: _lib.SD_F16}
+
+KIND = {"greedy": _lib.SD_PROC_GREEDY, "multinomial": _lib.SD_PROC_MULTINOMIAL, "topk": _lib.SD_PROC_TOPK,
+        "nucleus": _lib.SD_PROC_NUCLEUS, "topknucleus": _lib.SD_PROC_TOPK_NUCLEUS}
+# the reference's class names (utils/logits_processor.py) and ours map to the same kinds
+_CLASS_KIND = {"GreedyProcessor": "greedy", "MultinomialProcessor": "multinomial", "TopKProcessor": "topk",
+               "NucleusProcessor": "nucleus", "TopKNucleusProcessor": "topknucleus"}
+
+
+@dataclass(frozen=True)
+class ProcSpec:
+    kind: str = "greedy"
+    temperature: float = 1.0
+    top_k: int = 0
+    top_p: float = 1.0
+
+    @property
+    def stochastic(self) -> bool:
+        return self.kind != "greedy"
+
+    def struct(self) -> _lib.sd_processor:
+        return _lib.sd_processor(KIND[self.kind], float(self.temperature), int(self.top_k), float(self.top_p))
+
+
+PLAIN_SOFTMAX = ProcSpec("multinomial", 1.0)   # engine/infer_engine.py:241,276 (T=1, no processor)
+
+
+def proc_spec(proc) -> ProcSpec:
+    """ProcSpec of one of the five processors (ours, the reference's, or a ProcSpec)."""
+    if isinstance(proc, ProcSpec):
+        return proc
+    name = type(proc).__name__
+    for cls in type(proc).__mro__:
+        if cls.__name__ in _CLASS_KIND:
+            name = cls.__name__
+            break
+    if name not in _CLASS_KIND:
+        raise TypeError(f"unsupported logits processor {type(proc).__name__}")
+    return ProcSpec(_CLASS_KIND[name], float(getattr(proc, "temperature", 1.0)),
+                    int(getattr(proc, "top_k", 0)), float(getattr(proc, "top_p", 1.0)))
+
+
+def _stream_ptr(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+_WS: Dict[torch.device, torch.Tensor] = {}
+
+
+def _workspace(nbytes: int, device) -> torch.Tensor:
+    dev = torch.device(device)
+    ws = _WS.get(dev)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+        _WS[dev] = ws
+    return ws
+
+
+def _require_rows(t: torch.Tensor, name: str, V: int) -> None:
+    if t.dim() != 2 or t.shape[1] != V:
+        raise ValueError(f"{name}: expected [rows, {V}], got {tuple(t.shape)}")
+    if t.stride(1) != 1:
+        raise ValueError(f"{name}: vocab axis must be contiguous")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a device tensor")
+    if t.dtype not in _DT:
+        raise ValueError(f"{name}: unsupported dtype {t.dtype}")
+
+
+def _noise_struct(noise, n_words_needed: int, device):
+    """(sd_noise, keepalive tensor) for a call that may consume up to n_words_needed words."""
+    if isinstance(noise, StreamNoise):
+        words = noise.draw(n_words_needed, device)
+        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0), words
+    if isinstance(noise, PhiloxNoise):
+        return _lib.sd_noise(_lib.SD_NOISE_PHILOX, None, 0, noise.seed, noise.next_offset()), None
+    raise TypeError(f"unsupported noise source {type(noise).__name__}")
+
+
+# --------------------------------------------------------------------------- sampling
+def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Tensor] = None,
+                want_prob: bool = False):
+    """LogitsProcessor.__call__ + .sample on every row of logits [R, V] (one sample per row).
+
+    Returns (tokens int64 [R], token_prob fp32 [R] or None, row_status int32 [R]).  Under
+    StreamNoise the generator advances by 2·R·V words (torch.multinomial's Exp noise).
+    """
+    spec = proc_spec(proc)
+    R, V = logits.shape
+    _require_rows(logits, "logits", V)
+    dev = logits.device
+    tokens = tokens_out if tokens_out is not None else torch.empty(R, dtype=torch.long, device=dev)
+    if tokens.dtype != torch.long or tokens.numel() < R or not tokens.is_cuda:
+        raise ValueError("tokens_out must be an int64 device tensor with >= rows elements")
+    prob = torch.empty(R, dtype=torch.float32, device=dev) if want_prob else None
+    status = torch.empty(R, dtype=torch.int32, device=dev)
+    need = 2 * R * V if spec.stochastic else 0
+    nz, keep = _noise_struct(noise, need, dev)
+    nbytes = lib.sd_sample_workspace_size(R, V)
+    ws = _workspace(nbytes, dev)
+    a = _lib.sd_sample_args(R, V, logits.data_ptr(), logits.stride(0), _DT[logits.dtype], spec.struct(), nz,
+                            tokens.data_ptr(), tokens.stride(0) if tokens.dim() == 1 else 1,
+                            prob.data_ptr() if prob is not None else None, status.data_ptr(), None,
+                            ws.data_ptr(), ws.numel())
+    _lib.check(lib.sd_sample(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_sample")
+    if isinstance(noise, StreamNoise):
+        noise.advance(need)
+    del keep
+    return tokens, prob, status
+
+
+def probs_rows(logits: torch.Tensor, proc) -> torch.Tensor:
+    """LogitsProcessor.__call__: softmax(_process(logits) / T) in the logits dtype, on the device."""
+    spec = proc_spec(proc)
+    shape = logits.shape
+    x = logits.reshape(-1, shape[-1])
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    R, V = x.shape
+    _require_rows(x, "logits", V)
+    out = torch.empty((R, V), dtype=x.dtype, device=x.device)
+    ws = _workspace(lib.sd_probs_workspace_size(R, V), x.device)
+    a = _lib.sd_probs_args(R, V, x.data_ptr(), x.stride(0), _DT[x.dtype], spec.struct(), out.data_ptr(),
+                           out.stride(0), ws.data_ptr(), ws.numel())
+    _lib.check(lib.sd_probs(C.byref(a), C.c_void_p(_stream_ptr(x.device))), "sd_probs")
+    return out.reshape(shape)
+
+
+# --------------------------------------------------------------------------- verify
+@dataclass
+class VerifyOut:
+    n_accepted: torch.Tensor      # int32 [B]
+    next_token: torch.Tensor      # int64 [B]
+    resample_mass: torch.Tensor   # fp32  [B]
+    prune_drafter: torch.Tensor   # int32 [B]
+    prune_target: torch.Tensor    # int32 [B]
+    stop_index: torch.Tensor      # int32 [B]
+    row_status: torch.Tensor      # int32 [B]
+    words_used: torch.Tensor      # int64 [1]
+
+
+def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tensor], draft_tokens: torch.Tensor,
+           rule: int, target_proc, draft_proc, noise, stop_tokens: Optional[torch.Tensor] = None,
+           skip_sample_adjustment: bool = False, draft_is_probs: bool = False,
+           active: Optional[torch.Tensor] = None, engine_state: Optional[dict] = None,
+           sync_noise: bool = True) -> VerifyOut:
+    """One verify step for B sequences.
+
+    target_rows: γ+1 (SPEC) or γ (ENGINE) tensors [B, V] — row t of every sequence;
+    draft_rows:  γ tensors [B, V] (logits, or fp32 probabilities with draft_is_probs);
+    draft_tokens: int64 [B, >=γ].  Under StreamNoise the torch generator is advanced by the
+    words the kernels consumed, which needs one device->host read (sync_noise).
+    """
+    gamma = len(draft_rows)
+    if not 1 <= gamma <= _lib.SD_MAX_GAMMA:
+        raise ValueError(f"gamma must be in [1, {_lib.SD_MAX_GAMMA}], got {gamma}")
+    n_t = gamma + 1 if rule == _lib.SD_RULE_SPEC else gamma
+    if len(target_rows) != n_t:
+        raise ValueError(f"expected {n_t} target rows, got {len(target_rows)}")
+    B, V = target_rows[0].shape
+    dev = target_rows[0].device
+    tdt = target_rows[0].dtype
+    # the batch stride is shared by a row set (it is irrelevant when B == 1)
+    t_stride = target_rows[0].stride(0) if B > 1 else 0
+    d_stride = draft_rows[0].stride(0) if B > 1 else 0
+    for i, t in enumerate(target_rows):
+        _require_rows(t, f"target_rows[{i}]", V)
+        if t.shape[0] != B or t.dtype != tdt or (B > 1 and t.stride(0) != t_stride) or t.device != dev:
+            raise ValueError("target rows must share batch, dtype, batch stride and device")
+    for i, d in enumerate(draft_rows):
+        _require_rows(d, f"draft_rows[{i}]", V)
+        if d.shape[0] != B or d.dtype != draft_rows[0].dtype or (B > 1 and d.stride(0) != d_stride) \
+                or d.device != dev:
+            raise ValueError("draft rows must share batch, dtype, batch stride and device")
+    if draft_is_probs and draft_rows[0].dtype != torch.float32:
+        raise ValueError("draft probabilities must be fp32")
+    if draft_tokens.dtype != torch.long or draft_tokens.dim() != 2 or draft_tokens.shape[0] != B \
+            or draft_tokens.shape[1] < gamma or draft_tokens.stride(1) != 1 or draft_tokens.device != dev:
+        raise ValueError(f"draft_tokens must be int64 [B, >={gamma}] on {dev}")
+    tspec, dspec = proc_spec(target_proc), proc_spec(draft_proc)
+    stops = stop_tokens if stop_tokens is not None else torch.empty(0, dtype=torch.long, device=dev)
+    if stops.dtype != torch.long or stops.device != dev:
+        raise ValueError("stop_tokens must be an int64 device tensor")
+    if active is not None and (active.dtype not in (torch.uint8, torch.bool) or active.numel() != B):
+        raise ValueError("active must be uint8/bool [B]")
+
+    i32 = dict(dtype=torch.int32, device=dev)
+    out = VerifyOut(torch.empty(B, **i32), torch.empty(B, dtype=torch.long, device=dev),
+                    torch.empty(B, dtype=torch.float32, device=dev), torch.zeros(B, **i32),
+                    torch.zeros(B, **i32), torch.empty(B, **i32), torch.empty(B, **i32),
+                    torch.zeros(1, dtype=torch.long, device=dev))
+    stochastic = rule == _lib.SD_RULE_ENGINE or tspec.stochastic
+    need = B * (gamma + (2 * V if stochastic else 0))
+    nz, keep = _noise_struct(noise, need, dev)
+    ws = _workspace(lib.sd_verify_workspace_size(B, gamma, V), dev)
+
+    a = _lib.sd_verify_args()
+    a.batch, a.gamma, a.vocab, a.rule = B, gamma, V, rule
+    for i, t in enumerate(target_rows):
+        a.target_rows[i] = t.data_ptr()
+    a.target_stride_b, a.target_dtype = t_stride, _DT[tdt]
+    for i, d in enumerate(draft_rows):
+        a.draft_rows[i] = d.data_ptr()
+    a.draft_stride_b, a.draft_dtype = d_stride, _DT[draft_rows[0].dtype]
+    a.draft_is_probs = int(draft_is_probs)
+    a.draft_tokens, a.draft_tokens_stride_b = draft_tokens.data_ptr(), draft_tokens.stride(0)
+    a.target_proc, a.draft_proc = tspec.struct(), dspec.struct()
+    a.skip_sample_adjustment = int(skip_sample_adjustment)
+    a.stop_tokens, a.n_stop = (stops.data_ptr() if stops.numel() else None), stops.numel()
+    a.active = active.data_ptr() if active is not None else None
+    a.noise = nz
+    a.n_accepted, a.next_token, a.resample_mass = out.n_accepted.data_ptr(), out.next_token.data_ptr(), \
+        out.resample_mass.data_ptr()
+    a.prune_drafter, a.prune_target = out.prune_drafter.data_ptr(), out.prune_target.data_ptr()
+    a.stop_index, a.row_status, a.words_used = out.stop_index.data_ptr(), out.row_status.data_ptr(), \
+        out.words_used.data_ptr()
+    if engine_state is not None:
+        gen, fin, acc = engine_state["generated"], engine_state["finished"], engine_state["accepted"]
+        if gen.dtype != torch.long or gen.shape[0] != B or gen.stride(1) != 1:
+            raise ValueError("engine generated must be int64 [B, gen_len]")
+        if engine_state["step"] + gamma > gen.shape[1]:
+            raise ValueError("engine step window exceeds generated length")
+        if fin.dtype not in (torch.uint8, torch.bool) or acc.dtype != torch.long:
+            raise ValueError("engine finished must be uint8/bool, accepted int64")
+        a.generated, a.generated_stride_b, a.step = gen.data_ptr(), gen.stride(0), int(engine_state["step"])
+        a.finished, a.accepted_count = fin.data_ptr(), acc.data_ptr()
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    _lib.check(lib.sd_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_verify")
+    if isinstance(noise, StreamNoise) and sync_noise:
+        noise.advance(int(out.words_used.item()))
+    del keep
+    return out

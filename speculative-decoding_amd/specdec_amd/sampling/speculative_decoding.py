@@ -1,0 +1,137 @@
+"""Batch-1 speculative sampling loop on the fused HIP path.
+
+Drop-in for sampling/speculative_decoding.py:22-189 (``speculative_generate``): same
+signature, defaults and return value ``(List[int], float)``.  Per step the drafter runs γ'
+forwards (PyTorch-ROCm); each draft row is processed + sampled by ``sd_sample`` straight into
+``input_ids`` on the device; the target runs once; then ONE ``sd_verify`` call does the
+processor softmax over the γ'+1 target and γ' drafter rows, the ``r <= p/q`` accept test, the
+stop-token scan, the bonus / (p-q)+ residual sample and the prune lengths.  The host reads
+back four integers per step.
+
+Differences from the reference, all on paths where it is broken: ``use_cache``
+works on transformers 5.x (only uncached positions are fed, caches are cropped on reject), and
+``debug`` printing is reduced to one line per step.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+from torch.nn import Module
+
+from .. import _lib
+from ..noise import default_noise
+from ..ops import proc_spec, sample_rows, verify
+from ..utils.caching import prune_cache
+from ..utils.logits_processor import GreedyProcessor, LogitsProcessor
+
+
+def max_fn(x: torch.Tensor) -> torch.Tensor:
+    """sampling/speculative_decoding.py:10-19 (x⁺ / Σx⁺).  The verify kernel fuses this; kept
+    as a tensor utility for callers of the reference API."""
+    x_max = torch.where(x > 0, x, torch.zeros_like(x))
+    return x_max / torch.sum(x_max, dim=-1, keepdim=True)
+
+
+def _cache_len(cache) -> int:
+    if cache is None:
+        return 0
+    if isinstance(cache, tuple):
+        return cache[0][0].shape[2]
+    if hasattr(cache, "get_seq_length"):
+        return int(cache.get_seq_length())
+    return int(cache.length)
+
+
+def _forward(model, ids: torch.Tensor, end: int, cache, use_cache: bool):
+    """Run `model` on positions [cached, end) of ids; returns (logits, new cache, first position)."""
+    start = _cache_len(cache) if use_cache else 0
+    out = model(input_ids=ids[..., start:end], past_key_values=cache if use_cache else None, use_cache=use_cache)
+    return out.logits, out.past_key_values, start
+
+
+@torch.no_grad()
+def speculative_generate(
+    inputs: List[int],
+    drafter: Module,
+    target: Module,
+    tokenizer=None,
+    gamma: int = 5,
+    logits_processor: LogitsProcessor = GreedyProcessor(),
+    max_gen_len: int = 40,
+    eos_tokens_id: int | List[int] = 1,
+    pad_token_id: int = 0,
+    use_cache: bool = False,
+    skip_sample_adjustment: bool = False,
+    first_target: bool = True,
+    debug: bool = False,
+) -> Tuple[List[int], float]:
+    spec = proc_spec(logits_processor)
+    noise = default_noise()
+    dev = target.device
+    if torch.device(dev).type != "cuda":
+        raise RuntimeError("specdec_amd.speculative_generate runs on the GPU (HIP); the target is on "
+                           f"{dev}. There is no CPU path.")
+    stops = eos_tokens_id if isinstance(eos_tokens_id, list) else [eos_tokens_id]
+    stop_t = torch.tensor(stops, dtype=torch.long, device=dev)
+    drafts_accepted, drafts_speculated = 0.0, 0.0                # :71
+    cfg = target.config
+    max_seq = getattr(cfg, "max_position_embeddings", None) or getattr(cfg, "max_context_length", None) or 1024
+    prompt_len = len(inputs)
+    total_len = min(max_seq, prompt_len + max_gen_len)           # :77-78
+    input_ids = torch.full((1, total_len), pad_token_id, dtype=torch.long, device=dev)
+    input_ids[0, :prompt_len] = torch.tensor(inputs, dtype=torch.long, device=dev)
+    cur = prompt_len
+    drafter_cache = target_cache = None
+
+    if first_target:                                             # :84-103
+        logits, target_cache, _ = _forward(target, input_ids, cur, target_cache, use_cache)
+        sample_rows(logits[:, -1, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1])
+        t = int(input_ids[0, cur].item())
+        cur += 1
+        if t in stops:
+            return input_ids[0, prompt_len:cur].tolist(), 0
+
+    while cur < total_len:                                       # :105
+        g = min(gamma, total_len - cur - 1)                      # :106
+        ids_d = input_ids.to(drafter.device)
+        draft_rows = []
+        for k in range(g):                                       # :112-124
+            logits, drafter_cache, _ = _forward(drafter, ids_d, cur + k, drafter_cache, use_cache)
+            row = logits[:, -1, :]
+            sample_rows(row, spec, noise, tokens_out=ids_d[0, cur + k:cur + k + 1])
+            draft_rows.append(row if row.device == torch.device(dev) else row.to(dev))
+        drafts_speculated += g
+        input_ids = ids_d.to(dev)
+        logits, target_cache, start = _forward(target, input_ids, cur + g, target_cache, use_cache)
+        if g == 0:
+            # last position: rand(0) draws nothing, n = 0 = γ', the bonus row is sampled (:158-171)
+            sample_rows(logits[:, cur - 1 - start, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1])
+            x = int(input_ids[0, cur].item())
+            cur += 1
+            if x in stops:
+                return input_ids[0, prompt_len:cur].tolist(), drafts_accepted / drafts_speculated
+            continue
+        trows = [logits[:, cur - 1 + t - start, :] for t in range(g + 1)]   # :135 and bonus row :159
+        out = verify(trows, draft_rows, input_ids[:, cur:cur + g], _lib.SD_RULE_SPEC, spec, spec, noise,
+                     stop_t, skip_sample_adjustment=skip_sample_adjustment)
+        n, x, status, stop_index = (int(v) for v in torch.stack([
+            out.n_accepted[0].long(), out.next_token[0], out.row_status[0].long(), out.stop_index[0].long()]).tolist())
+        if status & _lib.SD_ROW_INVALID_DIST:
+            raise RuntimeError("probability tensor contains either `inf`, `nan` or element < 0")
+        if status & _lib.SD_ROW_NOISE_OVERRUN:
+            raise RuntimeError("specdec: noise stream overrun")
+        drafts_accepted += n                                     # :147
+        if status & _lib.SD_ROW_STOP_IN_DRAFTS:                  # :150-155
+            return input_ids[0, prompt_len:cur + stop_index + 1].tolist(), drafts_accepted / drafts_speculated
+        if n < g and use_cache:                                  # :163-165
+            drafter_cache = prune_cache(drafter_cache, g - n)
+            target_cache = prune_cache(target_cache, g - n + 1)
+        input_ids[0, cur + n:cur + g] = pad_token_id             # :176-177
+        input_ids[0, cur + n] = x
+        if debug:
+            print(f"[specdec] pos {cur}: accepted {n}/{g}, next {x}")
+        cur += n + 1
+        if x in stops:                                           # :184-187
+            return input_ids[0, prompt_len:cur].tolist(), drafts_accepted / drafts_speculated
+    return input_ids[0, prompt_len:].tolist(), drafts_accepted / drafts_speculated

@@ -23,6 +23,12 @@ class FakeCache:
     def __init__(self, length: int):
         self.length = length
 
+    def get_seq_length(self) -> int:
+        return self.length
+
+    def crop(self, max_length: int) -> None:   # transformers-5 DynamicCache.crop
+        self.length = max_length
+
 
 class FakeLM:
     def __init__(self, bank: torch.Tensor, max_position_embeddings: int = 4096, pos_mult: int = 7):

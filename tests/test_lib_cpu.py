@@ -1,0 +1,111 @@
+"""CPU-side checks of the C ABI: the library loads, exports every symbol include/specdec.h
+declares, its ctypes mirror has the C layout, and the host mt19937 stream equals torch's."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "specdec.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int32_t|size_t|const char\*)\s+(sd_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from specdec_amd import _lib
+    names = declared_functions()
+    assert len(names) >= 10
+    for n in names:
+        assert hasattr(_lib.lib, n), n
+    assert set(names) == set(_lib.EXPORTS)
+    assert _lib.lib.sd_abi_version() == _lib.SD_ABI_VERSION
+
+
+C_LAYOUT = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "specdec.h"
+#define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("sd_verify_args %zu\n", sizeof(sd_verify_args));
+  printf("sd_sample_args %zu\n", sizeof(sd_sample_args));
+  printf("sd_probs_args %zu\n", sizeof(sd_probs_args));
+  printf("sd_noise %zu\n", sizeof(sd_noise));
+  F(sd_verify_args, draft_rows) F(sd_verify_args, draft_tokens) F(sd_verify_args, target_proc)
+  F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
+  F(sd_verify_args, step) F(sd_verify_args, workspace_bytes)
+  F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes)
+  F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes)
+  return 0;
+}
+"""
+
+
+def test_ctypes_layout_matches_c_header():
+    from specdec_amd import _lib
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "l.c"), os.path.join(d, "l")
+        open(src, "w").write(C_LAYOUT)
+        subprocess.check_call(["gcc", "-std=c11", "-I", os.path.dirname(HEADER), src, "-o", exe])
+        out = subprocess.check_output([exe]).decode().split("\n")
+    got = dict(line.rsplit(" ", 1) for line in out if line)
+    for name, cls in [("sd_verify_args", _lib.sd_verify_args), ("sd_sample_args", _lib.sd_sample_args),
+                      ("sd_probs_args", _lib.sd_probs_args), ("sd_noise", _lib.sd_noise)]:
+        assert int(got[name]) == C.sizeof(cls), name
+    for key, val in got.items():
+        if "." in key:
+            struct, field = key.split(".")
+            assert getattr(getattr(_lib, struct), field).offset == int(val), key
+
+
+def test_workspace_sizes_are_positive_and_reject_bad_shapes():
+    from specdec_amd._lib import lib
+    assert lib.sd_verify_workspace_size(32, 4, 128256) > 0
+    assert lib.sd_verify_workspace_size(0, 4, 128256) == 0
+    assert lib.sd_verify_workspace_size(1, 17, 128256) == 0
+    assert lib.sd_sample_workspace_size(4, 50257) > 0
+
+
+def test_verify_rejects_invalid_args_without_touching_the_gpu():
+    from specdec_amd import _lib
+    a = _lib.sd_verify_args()
+    a.batch, a.gamma, a.vocab = 1, 4, 100
+    assert _lib.lib.sd_verify(C.byref(a), None) == _lib.SD_ERR_INVALID   # null pointers
+    a.gamma = 99
+    assert _lib.lib.sd_verify(C.byref(a), None) == _lib.SD_ERR_INVALID
+
+
+@pytest.mark.parametrize("skip", [0, 3, 623, 624, 625, 5000])
+def test_mt19937_stream_equals_torch_draws(skip):
+    from specdec_amd.noise import StreamNoise
+    g = torch.Generator().manual_seed(1234)
+    torch.rand(skip, generator=g)
+    n = StreamNoise(g)
+    w = n.draw(4000, "cpu").numpy().view(np.uint32).astype(np.uint64)
+    ref = torch.Generator().manual_seed(1234)
+    torch.rand(skip, generator=ref)
+    r = torch.rand(1000, generator=ref).numpy()
+    assert np.array_equal(((w[:1000] & 0xFFFFFF) * 2.0 ** -24).astype(np.float32), r)
+    e = torch.empty(1500).exponential_(generator=ref).numpy()
+    u = (((w[1000:4000:2] << np.uint64(32)) | w[1001:4000:2]) & np.uint64((1 << 53) - 1)).astype(np.float64)
+    assert np.array_equal((-np.log1p(-u * 2.0 ** -53)).astype(np.float32), e)
+    n.advance(4000)
+    assert torch.equal(g.get_state(), ref.get_state())
+
+
+def test_mt19937_advance_large():
+    from specdec_amd.noise import StreamNoise
+    for k in (1, 624 * 3 + 7, 100_003):
+        g = torch.Generator().manual_seed(99)
+        StreamNoise(g).advance(k)
+        r = torch.Generator().manual_seed(99)
+        torch.rand(k, generator=r)
+        assert torch.equal(g.get_state(), r.get_state())
