@@ -155,6 +155,11 @@ typedef struct {
 
     void* workspace;
     size_t workspace_bytes;
+
+    /* optional instrumentation: hipEvent_t recorded on `stream` right before / after the
+       row-statistics kernel (the pass that reads every logit row once); nullable.          */
+    void* prof_stats_begin;
+    void* prof_stats_end;
 } sd_verify_args;
 
 typedef struct {
@@ -191,6 +196,7 @@ typedef struct {
 
 int32_t sd_abi_version(void);
 const char* sd_status_string(int32_t status);
+const char* sd_last_hip_error(void);   /* hipGetErrorString of the last failed launch (this thread) */
 
 size_t sd_verify_workspace_size(int32_t batch, int32_t gamma, int32_t vocab);
 int32_t sd_verify(const sd_verify_args* args, void* stream);

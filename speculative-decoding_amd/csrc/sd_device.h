@@ -59,6 +59,28 @@ __device__ __forceinline__ float load_dyn(int dt, const void* row, int64_t i) {
                         : (dt == SD_BF16 ? load_one<SD_BF16>(row, i) : load_one<SD_F16>(row, i));
 }
 
+// Unpack one 16-byte vector into kVec floats.
+template <int DT>
+__device__ __forceinline__ void unpack16(const uint4 w, float* out) {
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+    if constexpr (DT == SD_F32) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) out[k] = __uint_as_float(ws[k]);
+    } else if constexpr (DT == SD_BF16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            out[2 * k] = __uint_as_float(ws[k] << 16);
+            out[2 * k + 1] = __uint_as_float(ws[k] & 0xffff0000u);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            out[2 * k] = __half2float(__ushort_as_half((unsigned short)(ws[k] & 0xffffu)));
+            out[2 * k + 1] = __half2float(__ushort_as_half((unsigned short)(ws[k] >> 16)));
+        }
+    }
+}
+
 // Load one 16-byte vector (kVec elements) starting at element e0, or the in-range part of it.
 template <int DT>
 __device__ __forceinline__ void load_vec(const void* row, int64_t e0, int vocab, bool aligned, float* out) {
@@ -86,6 +108,20 @@ __device__ __forceinline__ void load_vec(const void* row, int64_t e0, int vocab,
 #pragma unroll
         for (int k = 0; k < V; ++k) out[k] = (e0 + k < vocab) ? load_one<DT>(row, e0 + k) : 0.f;
     }
+}
+
+// ---------------------------------------------------------------- exp
+// e^x with v_exp_f32 (2^t) and the rounding error of t = x*log2(e) folded back in by FMA:
+// ~1 ulp like ocml's expf but without its range/denormal branches.  Every kernel uses this
+// one function, so a row's normaliser and its probabilities are computed consistently.
+__device__ __forceinline__ float sd_exp(float x) {
+    constexpr float kL = 1.44269502162933349609375f;       // log2(e) rounded to fp32
+    constexpr float kLlo = 1.925963033500011e-08f;          // log2(e) - kL
+    x = x < -1000.f ? -1000.f : x;                          // -inf -> 0 (not inf-inf = NaN); NaN stays NaN
+    const float t = x * kL;
+    const float err = fmaf(x, kL, -t) + x * kLlo;           // x*log2(e) - t
+    const float r = __builtin_amdgcn_exp2f(t);
+    return fmaf(r, err * 0.693147180559945309f, r);
 }
 
 // ---------------------------------------------------------------- processors
@@ -177,6 +213,45 @@ __device__ __forceinline__ uint4 philox_block(const sd_noise& nz, uint32_t row, 
     const uint4 c = make_uint4(idx, (row & 0x00ffffffu) | (site << 24), (uint32_t)nz.offset,
                                (uint32_t)(nz.offset >> 32));
     return philox4x32_10(c, make_uint2((uint32_t)nz.seed, (uint32_t)(nz.seed >> 32)));
+}
+
+// perf-mode Exp(1) from one 32-bit word: u in (0,1) at 24 bits, E = -ln(u) in fp32
+__device__ __forceinline__ float exp1_from_word(uint32_t w) {
+    const float u = (float)(w >> 8) * 5.9604644775390625e-08f + 2.98023223876953125e-08f;
+    return -__logf(u);
+}
+
+// Exp(1) noise of element j of a sampled row.  STREAM: torch's exponential_ draw for element j
+// (2 words at woff + 2j).  PHILOX: word (j & 3) of block (row, sample, j >> 2).
+__device__ __forceinline__ float exp_noise(const sd_noise& nz, int64_t woff, int row, int64_t j) {
+    if (nz.mode == SD_NOISE_STREAM) {
+        const int64_t w = woff + 2 * j;
+        if (w + 1 >= nz.n_words) return 1.f;   // overrun is flagged by the caller
+        return exp1_from_words(nz.words[w], nz.words[w + 1]);
+    }
+    const uint4 q = philox_block(nz, (uint32_t)row, kSiteSample, (uint32_t)(j >> 2));
+    const uint32_t w = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;
+    return exp1_from_word(w);
+}
+
+// The same values for VEC consecutive elements starting at e0 (e0 % 4 == 0), vectorised; the
+// noise mode NZ is a compile-time parameter so perf-mode kernels carry no fp64 log1p code.
+template <int VEC, int NZ>
+__device__ __forceinline__ void exp_noise_vec(const sd_noise& nz, int64_t woff, int row, int64_t e0, int vocab,
+                                              float* out) {
+    if constexpr (NZ == SD_NOISE_STREAM) {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) out[k] = (e0 + k < vocab) ? exp_noise(nz, woff, row, e0 + k) : 1.f;
+    } else {
+#pragma unroll
+        for (int q = 0; q < VEC / 4; ++q) {
+            const uint4 r = philox_block(nz, (uint32_t)row, kSiteSample, (uint32_t)((e0 >> 2) + q));
+            out[4 * q + 0] = exp1_from_word(r.x);
+            out[4 * q + 1] = exp1_from_word(r.y);
+            out[4 * q + 2] = exp1_from_word(r.z);
+            out[4 * q + 3] = exp1_from_word(r.w);
+        }
+    }
 }
 
 }  // namespace sd

@@ -17,6 +17,7 @@
 
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 
 #include "sd_device.h"
 
@@ -49,6 +50,7 @@ struct ResPart {
 struct Plan {
     int32_t B, gamma, V, rule;
     int32_t n_tslots, n_dslots, slots, n_chunks, chunk;
+    int32_t rn_chunks, rchunk;   // chunking of the resample / sample passes
     int32_t tdt, ddt, draft_is_probs, skip_adj;
     int32_t t_keep, d_keep, t_stoch, n_stop;
     float tT, dT;
@@ -133,46 +135,113 @@ struct FMax { __device__ float operator()(float a, float b) const { return fmaxf
 struct FSum { __device__ float operator()(float a, float b) const { return a + b; } };
 
 // ------------------------------------------------------------------ k_stats
-// Per (chunk, row): max and Σexp of y = round_dt(_process(x)/T) over the chunk.
-template <int DT, int EPT>
-__device__ void stats_body(const Plan& P, const void* row, float T, bool has_keep, int r, int c) {
-    __shared__ float lds[8];
-    constexpr int VEC = Elem<DT>::kVec, NV = EPT / VEC;
-    const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-    const RowKeep kp = has_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    const int64_t base = (int64_t)c * P.chunk;
-    float y[EPT];
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-        load_vec<DT>(row, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, P.V, aligned, &y[v * VEC]);
-    float m = -INFINITY;
-#pragma unroll
-    for (int v = 0; v < NV; ++v)
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            const int64_t j = base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k;
-            const float t = process_value<DT>(y[v * VEC + k], j, T, has_keep, kp);
-            y[v * VEC + k] = (j < P.V) ? t : -INFINITY;
-            m = fmaxf(m, y[v * VEC + k]);
-        }
-    m = block_reduce(m, FMax(), lds);
-    float s = 0.f;
-    if (m > -INFINITY) {
-#pragma unroll
-        for (int k = 0; k < EPT; ++k) s += expf(y[k] - m);
-    }
-    s = block_reduce(s, FSum(), lds);
-    if (threadIdx.x == 0) P.part[(int64_t)r * P.n_chunks + c] = make_float2(m, s);
+// grid (span, row-of-group): running max / Σexp of y = round_dt(_process(x)/T) over one span of a
+// row, streamed through a 4-deep register pipeline (16 B per lane per stage, 16 KiB per
+// workgroup in flight) with an online rescaled sum, so loads stay in flight while exp() runs.
+constexpr int kPipe = 4;
+
+__device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
+    const float mn = fmaxf(m, m2);
+    if (mn == -INFINITY) return;
+    s = (m > -INFINITY ? s * sd_exp(m - mn) : 0.f) + (m2 > -INFINITY ? s2 * sd_exp(m2 - mn) : 0.f);
+    m = mn;
 }
 
-template <int EPT>
-__global__ void __launch_bounds__(kThreads) k_stats(Plan P) {
-    const int r = blockIdx.y, c = blockIdx.x;
-    int dt; float T; bool keep;
-    const void* row = row_ptr(P, r, &dt, &T, &keep);
-    if (dt == SD_BF16) stats_body<SD_BF16, EPT>(P, row, T, keep, r, c);
-    else if (dt == SD_F32) stats_body<SD_F32, EPT>(P, row, T, keep, r, c);
-    else stats_body<SD_F16, EPT>(P, row, T, keep, r, c);
+__device__ __forceinline__ const void* slot_row(const Plan& P, int b, int s) {
+    if (s < P.n_tslots)
+        return static_cast<const char*>(P.trow[s]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
+    return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
+}
+
+template <int DT, bool FAST>
+__global__ void __launch_bounds__(kThreads) k_stats(Plan P, int slot_lo, int slot_cnt) {
+    __shared__ float lm[4], ls[4];
+    constexpr int VEC = Elem<DT>::kVec;
+    constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
+    const int b = blockIdx.y / slot_cnt, s = slot_lo + blockIdx.y % slot_cnt;
+    const int r = b * P.slots + s;
+    const void* row = slot_row(P, b, s);
+    const bool is_t = s < P.n_tslots;
+    const float T = is_t ? P.tT : P.dT;
+    const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
+    const RowKeep kp = has_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const int64_t lo = (int64_t)blockIdx.x * P.chunk;
+    const int64_t hi = lo + P.chunk < P.V ? lo + P.chunk : P.V;
+    const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+    const int nit = (int)((hi - lo + STEP - 1) / STEP);
+    float m = -INFINITY, acc = 0.f;
+
+    // one rescale per vector (only when its max beats the running max), one exp per element
+    auto consume = [&](const float* x, int64_t e0) {
+        float y[VEC];
+        float vm = -INFINITY;
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            y[k] = (e0 + k < hi) ? (FAST ? x[k] : process_value<DT>(x[k], e0 + k, T, has_keep, kp)) : -INFINITY;
+            vm = fmaxf(vm, y[k]);
+        }
+        if (vm > m) {
+            acc = m > -INFINITY ? acc * sd_exp(m - vm) : 0.f;
+            m = vm;
+        }
+        if (m > -INFINITY) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) acc += sd_exp(y[k] - m);
+        }
+    };
+    // steady state: stages where every lane's 16-byte vector is in range.  Loads are issued
+    // unconditionally (the prefetch index is clamped), so the compiler keeps kPipe of them in
+    // flight with counted vmcnt waits instead of draining to vmcnt(0) each stage.
+    const int nfull = aligned ? (int)((hi - lo) / STEP) : 0;
+    if (nfull > 0) {
+        const uint4* vb = reinterpret_cast<const uint4*>(static_cast<const char*>(row) + lo * Elem<DT>::kBytes) +
+                          threadIdx.x;
+        uint4 buf[kPipe];
+#pragma unroll
+        for (int d = 0; d < kPipe; ++d) buf[d] = vb[(d < nfull ? d : nfull - 1) * kThreads];
+        int it = 0;
+        for (; it + kPipe <= nfull; it += kPipe) {
+#pragma unroll
+            for (int d = 0; d < kPipe; ++d) {
+                const uint4 v = buf[d];
+                const int nx = it + d + kPipe;
+                buf[d] = vb[(nx < nfull ? nx : nfull - 1) * kThreads];
+                float x[VEC];
+                unpack16<DT>(v, x);
+                consume(x, lo + ((int64_t)(it + d) * kThreads + threadIdx.x) * VEC);
+            }
+        }
+#pragma unroll
+        for (int d = 0; d < kPipe; ++d) {
+            if (it + d < nfull) {
+                float x[VEC];
+                unpack16<DT>(buf[d], x);
+                consume(x, lo + ((int64_t)(it + d) * kThreads + threadIdx.x) * VEC);
+            }
+        }
+    }
+    // ragged tail (and misaligned rows): guarded element loads
+    for (int it = nfull; it < nit; ++it) {
+        const int64_t e0 = lo + ((int64_t)it * kThreads + threadIdx.x) * VEC;
+        float x[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < hi) ? load_one<DT>(row, e0 + k) : 0.f;
+        consume(x, e0);
+    }
+    // workgroup combine (fixed order)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const float m2 = __shfl_xor(m, o, kWave), s2 = __shfl_xor(acc, o, kWave);
+        online_merge(m, acc, m2, s2);
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) { lm[w] = m; ls[w] = acc; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float M = lm[0], S = ls[0];
+        for (int k = 1; k < kThreads / kWave; ++k) online_merge(M, S, lm[k], ls[k]);
+        P.part[(int64_t)r * P.n_chunks + blockIdx.x] = make_float2(M, S);
+    }
 }
 
 // combine the chunk partials of row r (one wave)
@@ -185,7 +254,7 @@ __device__ __forceinline__ float2 combine_row(const Plan& P, int r) {
     // fixed-order sum: lane-strided partial sums, then a fixed butterfly
     float s = 0.f;
     for (int c = lane; c < P.n_chunks; c += kWave)
-        if (pr[c].x > -INFINITY) s += pr[c].y * expf(pr[c].x - m);
+        if (pr[c].x > -INFINITY) s += pr[c].y * sd_exp(pr[c].x - m);
     s = wave_sum(s);
     return make_float2(m, s);
 }
@@ -194,7 +263,7 @@ template <int DT>
 __device__ __forceinline__ float prob_at(const void* row, int64_t j, float T, bool has_keep, const RowKeep& kp,
                                          float2 ms) {
     const float y = process_value<DT>(load_one<DT>(row, j), j, T, has_keep, kp);
-    return round_dt<DT>(expf(y - ms.x) / ms.y);
+    return round_dt<DT>(sd_exp(y - ms.x) / ms.y);
 }
 
 __device__ __forceinline__ float prob_dyn(int dt, const void* row, int64_t j, float T, bool has_keep,
@@ -204,40 +273,56 @@ __device__ __forceinline__ float prob_dyn(int dt, const void* row, int64_t j, fl
     return prob_at<SD_F16>(row, j, T, has_keep, kp, ms);
 }
 
-// ------------------------------------------------------------------ k_decide
-// grid (B), one wave: row stats for every slot of sequence b, then p(x_i), q(x_i).
-__global__ void __launch_bounds__(64) k_decide(Plan P) {
-    const int b = blockIdx.x, lane = threadIdx.x;
-    for (int s = 0; s < P.slots; ++s) {
+// ------------------------------------------------------------------ decide (row stats, p/q, walk)
+// Row statistics of every slot of sequence b, combined from the k_stats partials into LDS
+// (all waves of the block).  Stats stay in LDS for the block's own use: re-reading them from
+// global memory after a barrier could hit a line another block on this CU cached earlier.
+__device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int s = w; s < P.slots; s += nw) {
         const float2 ms = combine_row(P, b * P.slots + s);
-        if (lane == 0) P.rowstat[b * P.slots + s] = ms;
-    }
-    __syncthreads();
-    if (lane < P.gamma) {
-        const int i = lane;
-        const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
-        int dt; float T; bool keep;
-        const int rt = b * P.slots + i;
-        const void* trow = row_ptr(P, rt, &dt, &T, &keep);
-        const RowKeep kt = keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-        float p = 0.f, q = 0.f;
-        if (tok >= 0 && tok < P.V) {
-            p = prob_dyn(dt, trow, tok, T, keep, kt, P.rowstat[rt]);
-            if (P.draft_is_probs) {
-                q = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
-            } else {
-                const int rd = b * P.slots + P.n_tslots + i;
-                const void* drow = row_ptr(P, rd, &dt, &T, &keep);
-                const RowKeep kd = keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-                q = prob_dyn(dt, drow, tok, T, keep, kd, P.rowstat[rd]);
-            }
+        if (lane == 0) {
+            lstat[s] = ms;
+            if (publish) P.rowstat[b * P.slots + s] = ms;   // read by later launches only
         }
-        P.rp[b * P.gamma + i] = p;
-        P.rq[b * P.gamma + i] = q;
     }
 }
 
-// ------------------------------------------------------------------ k_walk
+// p(x_i), q(x_i) of the γ drafts (threads < γ; call after seq_stats + barrier)
+__device__ void seq_ratios(const Plan& P, int b, const float2* lstat, float* lp, float* lq) {
+    if (threadIdx.x >= P.gamma) return;
+    const int i = threadIdx.x;
+    const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
+    int dt; float T; bool keep;
+    const int rt = b * P.slots + i;
+    const void* trow = row_ptr(P, rt, &dt, &T, &keep);
+    const RowKeep kt = keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    float p = 0.f, q = 0.f;
+    if (tok >= 0 && tok < P.V) {
+        p = prob_dyn(dt, trow, tok, T, keep, kt, lstat[i]);
+        if (P.draft_is_probs) {
+            q = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
+        } else {
+            const int rd = b * P.slots + P.n_tslots + i;
+            const void* drow = row_ptr(P, rd, &dt, &T, &keep);
+            const RowKeep kd = keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+            q = prob_dyn(dt, drow, tok, T, keep, kd, lstat[P.n_tslots + i]);
+        }
+    }
+    lp[i] = p;
+    lq[i] = q;
+}
+
+// grid (B): STREAM-mode stage 1 — row stats and p/q ratios to global memory for the serial walk.
+__global__ void __launch_bounds__(256) k_decide(Plan P) {
+    __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
+    const int b = blockIdx.x;
+    seq_stats(P, b, lstat, true);
+    __syncthreads();
+    seq_ratios(P, b, lstat, P.rp + b * P.gamma, P.rq + b * P.gamma);
+}
+
+// ------------------------------------------------------------------ walk
 __device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64_t woff, bool* overrun) {
     if (P.noise.mode == SD_NOISE_STREAM) {
         if (woff >= P.noise.n_words) { *overrun = true; return 0.f; }
@@ -246,8 +331,8 @@ __device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64
     return uniform_from_word(philox_block(P.noise, (uint32_t)b, kSiteAccept, (uint32_t)i).x);
 }
 
-// Walk one sequence; returns words consumed (STREAM).  woff = first word of this sequence.
-__device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
+// The accept rule for one sequence given p(x_i), q(x_i); woff = its first noise word (STREAM).
+__device__ Decision walk_core(const Plan& P, int b, const float* rp, const float* rq, int64_t woff, int64_t* used_out) {
     Decision d{};
     d.stop_index = -1;
     d.noise_off = 0;
@@ -260,7 +345,7 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
         int n = g;
         for (int i = 0; i < g; ++i) {
             const float r = draw_uniform(P, b, i, woff + i, &overrun);
-            const float frac = P.rp[b * g + i] / P.rq[b * g + i];
+            const float frac = rp[i] / rq[i];
             if (r > frac && n == g) n = i;
         }
         used = g;
@@ -278,8 +363,6 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
             d.noise_off = woff + used;
             if (P.t_stoch) used += sample_words;
         }
-        if (P.prune_drafter) P.prune_drafter[b] = (n < g && d.stop_index < 0) ? g - n : 0;
-        if (P.prune_target) P.prune_target[b] = (n < g && d.stop_index < 0) ? g - n + 1 : 0;
     } else {
         // engine/infer_engine.py:287-330
         const bool act = P.active == nullptr || P.active[b] != 0;
@@ -289,7 +372,7 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
             d.status = SD_ROW_DONE;
             for (int i = 0; i < g; ++i) {
                 const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
-                const double p = P.rp[b * g + i], q = P.rq[b * g + i];
+                const double p = rp[i], q = rq[i];
                 const double ap = q <= 0.0 ? 1.0 : fmin(1.0, p / q);
                 const float u = draw_uniform(P, b, i, woff + used, &overrun);
                 used += 1;
@@ -310,9 +393,24 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
     if (overrun || (P.noise.mode == SD_NOISE_STREAM && d.mode != kModeNone && P.t_stoch &&
                     d.noise_off + sample_words > P.noise.n_words))
         d.status |= SD_ROW_NOISE_OVERRUN;
+    *used_out = used;
+    return d;
+}
+
+__device__ void publish_decision(const Plan& P, int b, const Decision& d) {
+    const int g = P.gamma;
+    const bool pruned = P.rule == SD_RULE_SPEC && d.n < g && d.stop_index < 0;   // the engine never prunes
+    if (P.prune_drafter) P.prune_drafter[b] = pruned ? g - d.n : 0;
+    if (P.prune_target) P.prune_target[b] = pruned ? g - d.n + 1 : 0;
     P.dec[b] = d;
     P.n_accepted[b] = d.n;
     if (P.stop_index) P.stop_index[b] = d.stop_index;
+}
+
+__device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
+    int64_t used;
+    const Decision d = walk_core(P, b, P.rp + b * P.gamma, P.rq + b * P.gamma, woff, &used);
+    publish_decision(P, b, d);
     return used;
 }
 
@@ -330,24 +428,14 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
     }
 }
 
-// ------------------------------------------------------------------ noise per element
-__device__ __forceinline__ float exp_noise(const sd_noise& nz, int64_t woff, int row, int64_t j) {
-    if (nz.mode == SD_NOISE_STREAM) {
-        const int64_t w = woff + 2 * j;
-        if (w + 1 >= nz.n_words) return 1.f;   // overrun is flagged by the walk
-        return exp1_from_words(nz.words[w], nz.words[w + 1]);
-    }
-    const uint4 q = philox_block(nz, (uint32_t)row, kSiteSample, (uint32_t)(j >> 1));
-    return (j & 1) ? exp1_from_words(q.z, q.w) : exp1_from_words(q.x, q.y);
-}
-
 // ------------------------------------------------------------------ k_resample
-// grid (chunk, B).  RESID: residual sum + argmax candidates; BONUS / PROW: argmax of the
-// multinomial (or greedy) value over the processed target row.
-template <int TDT, int DDT, int EPT>
-__device__ void resample_body(const Plan& P, const Decision& d, int b, int c) {
+// grid (chunk, B).  RESID: Σ(p_n - q_n)+ and the argmax candidates of fl(fl(res/S)/E) in one pass
+// over the two rows; BONUS / PROW: argmax of the multinomial (or greedy) value of the target row.
+constexpr float kCandTol = 1.0f - 16.0f * 5.9604645e-08f;   // candidates within 16 ulp of the max
+
+template <int TDT, int DDT, int NZ, int EPT>
+__device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float2 mst, float2 msd_in) {
     __shared__ float ldsf[8];
-    __shared__ int32_t ldsi[8];
     __shared__ int32_t lcount;
     __shared__ float lres[kMaxCand], le[kMaxCand];
     __shared__ int32_t lidx[kMaxCand];
@@ -357,114 +445,152 @@ __device__ void resample_body(const Plan& P, const Decision& d, int b, int c) {
     const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
     const bool t_al = (reinterpret_cast<uintptr_t>(trow) & 15) == 0;
     const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    const float2 mst = P.rowstat[rt];
-    const bool resid = d.mode == kModeResid;
     const bool stoch = P.t_stoch != 0;
-    const int64_t base = (int64_t)c * P.chunk;
-
-    const void* drow = nullptr;
-    bool d_al = false;
+    const int64_t base = (int64_t)c * P.rchunk;
+    const void* drow;
     RowKeep kd{-INFINITY, INT_MAX, 0, 0};
-    float2 msd = make_float2(0.f, 1.f);
-    if (resid) {
-        if (P.draft_is_probs) {
-            drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
-        } else {
-            const int rd = b * P.slots + P.n_tslots + d.slot;
-            drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
-            if (P.d_keep) kd = P.keep[rd];
-            msd = P.rowstat[rd];
-        }
-        d_al = (reinterpret_cast<uintptr_t>(drow) & 15) == 0;
+    const float2 msd = msd_in;
+    if (P.draft_is_probs) {
+        drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
+    } else {
+        const int rd = b * P.slots + P.n_tslots + d.slot;
+        drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
+        if (P.d_keep) kd = P.keep[rd];
     }
+    const bool d_al = (reinterpret_cast<uintptr_t>(drow) & 15) == 0;
 
     float sum = 0.f, wmax = 0.f;
-    float pv = -INFINITY;      // argmax (value, idx) of the p-based sample
-    int32_t pi = INT_MAX;
     float res[EPT], ev[EPT];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
-        float xt[VEC], xd[VEC];
+        float xt[VEC], xd[VEC], e[VEC];
         load_vec<TDT>(trow, e0, P.V, t_al, xt);
-        if (resid) {
-            if (P.draft_is_probs) load_vec<SD_F32>(drow, e0, P.V, d_al, xd);
-            else load_vec<DDT>(drow, e0, P.V, d_al, xd);
-        }
+        if (P.draft_is_probs) load_vec<SD_F32>(drow, e0, P.V, d_al, xd);
+        else load_vec<DDT>(drow, e0, P.V, d_al, xd);
+        if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
-            const int idx = v * VEC + k;
-            res[idx] = 0.f;
-            ev[idx] = 1.f;
-            if (j >= P.V) continue;
-            const float p = round_dt<TDT>(expf(process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt) - mst.x) / mst.y);
-            const float e = stoch ? exp_noise(P.noise, d.noise_off, b, j) : 1.f;
-            ev[idx] = e;
-            if (resid) {
-                const float q = P.draft_is_probs
-                    ? xd[k]
-                    : round_dt<DDT>(expf(process_value<DDT>(xd[k], j, P.dT, P.d_keep, kd) - msd.x) / msd.y);
-                const float diff = p - q;                          // bf16/fp32 - fp32 -> fp32
-                const float rr = diff > 0.f ? diff : 0.f;          // max_fn numerator / clamp(p - min(p,q), 0)
-                res[idx] = rr;
-                sum += rr;
-                const float w = rr / e;
-                wmax = fmaxf(wmax, w);
+            const float p = round_dt<TDT>(sd_exp(process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt) - mst.x) / mst.y);
+            const float q = P.draft_is_probs
+                ? xd[k]
+                : round_dt<DDT>(sd_exp(process_value<DDT>(xd[k], j, P.dT, P.d_keep, kd) - msd.x) / msd.y);
+            const float diff = p - q;                                 // bf16/fp32 - fp32 -> fp32
+            const float rr = (j < P.V && diff > 0.f) ? diff : 0.f;     // max_fn numerator, :317 clamp
+            res[v * VEC + k] = rr;
+            ev[v * VEC + k] = stoch ? e[k] : 1.f;
+            sum += rr;
+            wmax = fmaxf(wmax, stoch ? rr * __builtin_amdgcn_rcpf(e[k]) : rr);
+        }
+    }
+    const float bsum = block_reduce(sum, FSum(), ldsf);
+    const float bw = block_reduce(wmax, FMax(), ldsf);
+    if (threadIdx.x == 0) lcount = 0;
+    __syncthreads();
+    // any j whose exact fl(fl(res/S)/E) can tie the maximum has res/E within a few ulp of it
+    const float thr = bw * kCandTol;
+    if (bw > 0.f) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                const int idx = v * VEC + k;
+                const float w = stoch ? res[idx] * __builtin_amdgcn_rcpf(ev[idx]) : res[idx];
+                if (res[idx] > 0.f && w >= thr) {
+                    const int slot = atomicAdd(&lcount, 1);
+                    if (slot < kMaxCand) {
+                        lres[slot] = res[idx];
+                        le[slot] = ev[idx];
+                        lidx[slot] = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k);
+                    }
+                }
             }
-            // p-based sample value: bonus / p-row, or the engine's den<=1e-12 fallback
-            const float val = stoch ? round_dt<TDT>(p / round_dt<TDT>(e)) : p;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
+        o.sum = bsum;
+        o.wmax = bw;
+        o.ncand = lcount;
+        for (int k = 0; k < kMaxCand && k < lcount; ++k) { o.cres[k] = lres[k]; o.ce[k] = le[k]; o.cidx[k] = lidx[k]; }
+    }
+}
+
+template <int TDT, int NZ, int EPT>
+__device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2 mst) {
+    __shared__ float ldsf[8];
+    __shared__ int32_t ldsi[8];
+    constexpr int VEC = Elem<TDT>::kVec, NV = EPT / VEC;
+    const int rt = b * P.slots + d.slot;
+    const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
+    const bool t_al = (reinterpret_cast<uintptr_t>(trow) & 15) == 0;
+    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const bool stoch = P.t_stoch != 0;
+    const int64_t base = (int64_t)c * P.rchunk;
+    float pv = -INFINITY;
+    int32_t pi = INT_MAX;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+        float xt[VEC], e[VEC];
+        load_vec<TDT>(trow, e0, P.V, t_al, xt);
+        if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int64_t j = e0 + k;
+            if (j >= P.V) continue;
+            const float p = round_dt<TDT>(sd_exp(process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt) - mst.x) / mst.y);
+            const float val = stoch ? round_dt<TDT>(p / round_dt<TDT>(e[k])) : p;   // multinomial / argmax
             if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
         }
     }
     block_argmax(pv, pi, ldsf, ldsi);
-    float bsum = 0.f, bw = 0.f;
-    if (resid) {
-        bsum = block_reduce(sum, FSum(), ldsf);
-        bw = block_reduce(wmax, FMax(), ldsf);
-        if (threadIdx.x == 0) lcount = 0;
-        __syncthreads();
-        // candidates: any j whose exact value fl(fl(res/S)/E) can equal the max must have
-        // res/E within two fp32 roundings (plus this division's) of the max.
-        const float thr = bw * (1.0f - 4.0f * 5.9604645e-08f);
-        if (bw > 0.f) {
-#pragma unroll
-            for (int v = 0; v < NV; ++v)
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) {
-                    const int idx = v * VEC + k;
-                    const int64_t j = base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k;
-                    if (res[idx] > 0.f && res[idx] / ev[idx] >= thr) {
-                        const int slot = atomicAdd(&lcount, 1);
-                        if (slot < kMaxCand) { lres[slot] = res[idx]; le[slot] = ev[idx]; lidx[slot] = (int32_t)j; }
-                    }
-                }
-        }
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        ResPart& o = P.rpart[(int64_t)b * P.n_chunks + c];
+        ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
         o.pval = pv;
         o.pidx = pi;
-        o.sum = bsum;
-        o.wmax = bw;
-        o.ncand = resid ? lcount : 0;
-        if (resid)
-            for (int k = 0; k < kMaxCand && k < lcount; ++k) { o.cres[k] = lres[k]; o.ce[k] = le[k]; o.cidx[k] = lidx[k]; }
     }
 }
 
-template <int EPT>
+// FUSED (perf mode): every workgroup of sequence b first re-derives the decision itself — row
+// stats from the k_stats partials, p(x_i)/q(x_i), the accept walk on Philox uniforms — which is
+// cheap next to a kernel boundary; chunk 0 publishes it for k_finalize.  STREAM (parity) mode
+// reads the decision of the serial k_decide -> k_walk stages instead.
+template <int TDT, int DDT, int NZ, bool FUSED>
 __global__ void __launch_bounds__(kThreads) k_resample(Plan P) {
+    __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
+    __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
+    __shared__ Decision ldec;
     const int b = blockIdx.y, c = blockIdx.x;
-    const Decision d = P.dec[b];
-    if (d.mode == kModeNone || (d.status & SD_ROW_NOISE_OVERRUN)) return;
-    const int td = P.tdt, dd = P.draft_is_probs ? SD_F32 : P.ddt;
-#define SD_RS(T, D) if (td == T && dd == D) { resample_body<T, D, EPT>(P, d, b, c); return; }
-    SD_RS(SD_BF16, SD_BF16) SD_RS(SD_F32, SD_F32) SD_RS(SD_BF16, SD_F32) SD_RS(SD_F32, SD_BF16)
-    SD_RS(SD_F16, SD_F16) SD_RS(SD_F16, SD_F32) SD_RS(SD_BF16, SD_F16) SD_RS(SD_F16, SD_BF16)
-    SD_RS(SD_F32, SD_F16)
-#undef SD_RS
+    Decision d;
+    float2 mst, msd = make_float2(0.f, 1.f);
+    if constexpr (FUSED) {
+        seq_stats(P, b, lstat, c == 0);
+        __syncthreads();
+        seq_ratios(P, b, lstat, lp, lq);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int64_t used;
+            ldec = walk_core(P, b, lp, lq, 0, &used);
+            if (c == 0) {
+                publish_decision(P, b, ldec);
+                if (P.words_used && b == 0) *P.words_used = 0;
+            }
+        }
+        __syncthreads();
+        d = ldec;
+        if (d.mode == kModeNone) return;
+        mst = lstat[d.slot];
+        if (d.mode == kModeResid && !P.draft_is_probs) msd = lstat[P.n_tslots + d.slot];
+    } else {
+        d = P.dec[b];
+        if (d.mode == kModeNone || (d.status & SD_ROW_NOISE_OVERRUN)) return;
+        mst = P.rowstat[b * P.slots + d.slot];
+        if (d.mode == kModeResid && !P.draft_is_probs) msd = P.rowstat[b * P.slots + P.n_tslots + d.slot];
+    }
+    if (d.mode == kModeResid) resid_body<TDT, DDT, NZ, 8>(P, d, b, c, mst, msd);
+    else prow_body<TDT, NZ, 8>(P, d, b, c, mst);
 }
 
 // ------------------------------------------------------------------ k_finalize
@@ -477,27 +603,33 @@ __global__ void __launch_bounds__(64) k_finalize(Plan P) {
     float mass = NAN;
     int32_t status = d.status;
     if (d.mode != kModeNone && !(status & SD_ROW_NOISE_OVERRUN)) {
-        const ResPart* rp = P.rpart + (int64_t)b * P.n_chunks;
-        // p-based argmax across chunks (bonus / p-row / engine fallback)
-        float pv = -INFINITY;
-        int32_t pi = INT_MAX;
-        for (int c = lane; c < P.n_chunks; c += kWave)
-            if (arg_better(rp[c].pval, rp[c].pidx, pv, pi)) { pv = rp[c].pval; pi = rp[c].pidx; }
-        wave_argmax(pv, pi);
+        const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
         if (d.mode == kModeResid) {
-            // fixed-order residual sum (chunk order is lane-strided, then butterfly)
+            // fixed-order residual sum (lane-strided over chunks, then a fixed butterfly)
             float s = 0.f, wm = 0.f;
             int overflow = 0;
-            for (int c = lane; c < P.n_chunks; c += kWave) {
+            for (int c = lane; c < P.rn_chunks; c += kWave) {
                 s += rp[c].sum;
                 wm = fmaxf(wm, rp[c].wmax);
             }
             s = wave_sum(s);
             wm = wave_max(wm);
             mass = s;
-            const bool engine_fallback = (P.rule == SD_RULE_ENGINE) && ((double)s <= 1e-12);
-            if (engine_fallback) {
-                x = pi;
+            const int rt = b * P.slots + d.slot;
+            const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+            const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
+            const float2 mst = P.rowstat[rt];
+            if (P.rule == SD_RULE_ENGINE && (double)s <= 1e-12) {
+                // engine/infer_engine.py:319-321: multinomial(p) over the target row (rare: p ~= q)
+                float bv = -INFINITY;
+                int32_t bi = INT_MAX;
+                for (int64_t j = lane; j < P.V; j += kWave) {
+                    const float p = prob_dyn(P.tdt, trow, j, P.tT, P.t_keep, kt, mst);
+                    const float v = round_dyn(P.tdt, p / round_dyn(P.tdt, exp_noise(P.noise, d.noise_off, b, j)));
+                    if (arg_better(v, (int32_t)j, bv, bi)) { bv = v; bi = (int32_t)j; }
+                }
+                wave_argmax(bv, bi);
+                x = bi;
                 status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
             } else if (s == 0.f) {
                 // max_fn divides by zero: all-NaN distribution
@@ -505,10 +637,10 @@ __global__ void __launch_bounds__(64) k_finalize(Plan P) {
                 else x = 0;   // torch.argmax over an all-NaN row
             } else {
                 // exact evaluation of the candidates: v = fl(fl(res / S) / E)
-                const float thr = wm * (1.0f - 4.0f * 5.9604645e-08f);
+                const float thr = wm * kCandTol;
                 float bv = -INFINITY;
                 int32_t bi = INT_MAX;
-                for (int c = lane; c < P.n_chunks; c += kWave) {
+                for (int c = lane; c < P.rn_chunks; c += kWave) {
                     const ResPart& o = rp[c];
                     if (o.wmax < thr) continue;
                     if (o.ncand > kMaxCand) { overflow = 1; continue; }
@@ -519,13 +651,9 @@ __global__ void __launch_bounds__(64) k_finalize(Plan P) {
                     }
                 }
                 wave_argmax(bv, bi);
-                // overflowing chunks (many near-equal values, e.g. ties) are re-scanned exactly
+                // chunks with too many near-equal values (e.g. ties) are re-scanned exactly
                 overflow = __any(overflow);
                 if (overflow) {
-                    const int rt = b * P.slots + d.slot;
-                    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-                    const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
-                    const float2 mst = P.rowstat[rt];
                     const void* drow;
                     RowKeep kd{-INFINITY, INT_MAX, 0, 0};
                     float2 msd = make_float2(0.f, 1.f);
@@ -553,6 +681,12 @@ __global__ void __launch_bounds__(64) k_finalize(Plan P) {
                 x = bi;
             }
         } else {
+            // bonus / p-row: argmax across chunks
+            float pv = -INFINITY;
+            int32_t pi = INT_MAX;
+            for (int c = lane; c < P.rn_chunks; c += kWave)
+                if (arg_better(rp[c].pval, rp[c].pidx, pv, pi)) { pv = rp[c].pval; pi = rp[c].pidx; }
+            wave_argmax(pv, pi);
             x = pi;
         }
     }
@@ -584,7 +718,7 @@ __global__ void __launch_bounds__(64) k_finalize(Plan P) {
 
 // ------------------------------------------------------------------ sd_sample kernels
 // grid (chunk, R): argmax of round_dt(p / round_dt(E)) (multinomial) or p (greedy).
-template <int DT, int EPT>
+template <int DT, int NZ, int EPT>
 __device__ void rowsample_body(const Plan& P, int r, int c) {
     __shared__ float ldsf[8];
     __shared__ int32_t ldsi[8];
@@ -599,46 +733,44 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
     const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
     const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    const int64_t base = (int64_t)c * P.chunk;
+    const int64_t base = (int64_t)c * P.rchunk;
     const int64_t woff = 2ll * P.V * r;
     float pv = -INFINITY;
     int32_t pi = INT_MAX;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
-        float x[VEC];
+        float x[VEC], e[VEC];
         load_vec<DT>(row, e0, P.V, al, x);
+        if (P.t_stoch) exp_noise_vec<VEC, NZ>(P.noise, woff, r, e0, P.V, e);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = round_dt<DT>(expf(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
-            const float val = P.t_stoch ? round_dt<DT>(p / round_dt<DT>(exp_noise(P.noise, woff, r, j))) : p;
+            const float p = round_dt<DT>(sd_exp(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
+            const float val = P.t_stoch ? round_dt<DT>(p / round_dt<DT>(e[k])) : p;
             if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
         }
     }
     block_argmax(pv, pi, ldsf, ldsi);
     if (threadIdx.x == 0) {
-        ResPart& o = P.rpart[(int64_t)r * P.n_chunks + c];
+        ResPart& o = P.rpart[(int64_t)r * P.rn_chunks + c];
         o.pval = pv;
         o.pidx = pi;
     }
 }
 
-template <int EPT>
+template <int DT, int NZ>
 __global__ void __launch_bounds__(kThreads) k_rowsample(Plan P) {
-    const int r = blockIdx.y, c = blockIdx.x;
-    if (P.tdt == SD_BF16) rowsample_body<SD_BF16, EPT>(P, r, c);
-    else if (P.tdt == SD_F32) rowsample_body<SD_F32, EPT>(P, r, c);
-    else rowsample_body<SD_F16, EPT>(P, r, c);
+    rowsample_body<DT, NZ, 8>(P, blockIdx.y, blockIdx.x);
 }
 
 __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
     const int r = blockIdx.x, lane = threadIdx.x;
-    const ResPart* rp = P.rpart + (int64_t)r * P.n_chunks;
+    const ResPart* rp = P.rpart + (int64_t)r * P.rn_chunks;
     float pv = -INFINITY;
     int32_t pi = INT_MAX;
-    for (int c = lane; c < P.n_chunks; c += kWave)
+    for (int c = lane; c < P.rn_chunks; c += kWave)
         if (arg_better(rp[c].pval, rp[c].pidx, pv, pi)) { pv = rp[c].pval; pi = rp[c].pidx; }
     wave_argmax(pv, pi);
     const float2 ms = combine_row(P, r);
@@ -673,7 +805,7 @@ __device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r
     const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
     const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    const int64_t base = (int64_t)c * P.chunk;
+    const int64_t base = (int64_t)c * P.rchunk;
     char* orow = static_cast<char*>(out) + r * ostride * (DT == SD_F32 ? 4 : 2);
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -684,7 +816,7 @@ __device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = round_dt<DT>(expf(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
+            const float p = round_dt<DT>(sd_exp(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
             if constexpr (DT == SD_F32) reinterpret_cast<float*>(orow)[j] = p;
             else if constexpr (DT == SD_BF16) reinterpret_cast<uint16_t*>(orow)[j] = (uint16_t)(__float_as_uint(p) >> 16);
             else reinterpret_cast<__half*>(orow)[j] = __float2half_rn(p);
@@ -692,24 +824,25 @@ __device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r
     }
 }
 
-template <int EPT>
+template <int DT>
 __global__ void __launch_bounds__(kThreads) k_writeprobs(Plan P, void* out, int64_t ostride) {
-    const int r = blockIdx.y, c = blockIdx.x;
-    if (P.tdt == SD_BF16) writeprobs_body<SD_BF16, EPT>(P, out, ostride, r, c);
-    else if (P.tdt == SD_F32) writeprobs_body<SD_F32, EPT>(P, out, ostride, r, c);
-    else writeprobs_body<SD_F16, EPT>(P, out, ostride, r, c);
+    writeprobs_body<DT, 8>(P, out, ostride, blockIdx.y, blockIdx.x);
 }
 
 }  // namespace sd
 
 // ====================================================================== host side
+namespace {
+thread_local hipError_t g_last_error = hipSuccess;
+}  // namespace
+
 #include "sd_threshold.inc"
 
 namespace {
 
 using namespace sd;
 
-constexpr int kEptSmall = 8, kEptLarge = 32;
+constexpr int kEptSmall = 8;
 
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
@@ -746,22 +879,103 @@ bool valid_proc(const sd_processor& p) {
 }
 bool needs_keep(const sd_processor& p) { return p.kind >= SD_PROC_TOPK; }
 
-int choose_ept(int rows, int vocab) {
-    const int64_t big = (int64_t)rows * ((vocab + kThreads * kEptLarge - 1) / (kThreads * kEptLarge));
-    return big >= 2048 ? kEptLarge : kEptSmall;
+// Span of a k_stats workgroup: a multiple of one 2048-element stage, sized so the whole grid is
+// resident at once (<= 2048 workgroups = 256 CUs x 8): a grid a little over one residency
+// wave would run its remainder on 1/8 of the chip.  SD_STATS_STAGES overrides (tuning).
+void set_stats_chunks(sd::Plan& P, int rows) {
+    const int64_t stage = kThreads * 8;
+    const int64_t stages_per_row = (P.V + stage - 1) / stage;
+    int64_t per_wg = (rows * stages_per_row + 2047) / 2048;
+    if (const char* e = getenv("SD_STATS_STAGES")) per_wg = atoi(e);
+    per_wg = per_wg < 1 ? 1 : (per_wg > 16 ? 16 : per_wg);
+    P.chunk = (int32_t)(per_wg * stage);
+    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
 }
+
+void set_rchunks(sd::Plan& P) {
+    P.rchunk = kThreads * kEptSmall;
+    P.rn_chunks = (P.V + P.rchunk - 1) / P.rchunk;
+}
+
+int32_t launch_stats(const sd::Plan& P, void* stream);
 
 #define SD_LAUNCH(kern, grid, block, stream, ...)                                             \
     do {                                                                                      \
         hipLaunchKernelGGL(kern, grid, block, 0, (hipStream_t)stream, __VA_ARGS__);            \
-        if (hipGetLastError() != hipSuccess) return SD_ERR_LAUNCH;                            \
+        const hipError_t e_ = hipGetLastError();                                              \
+        if (e_ != hipSuccess) { g_last_error = e_; return SD_ERR_LAUNCH; }                    \
     } while (0)
+
+// errors left behind by earlier, unrelated runtime calls must not be blamed on our launches
+inline void clear_stale_error() { (void)hipGetLastError(); }
+
+template <int DT>
+int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt, void* stream) {
+    const dim3 grid(P.n_chunks, P.B * slot_cnt);
+    if (fast) SD_LAUNCH((k_stats<DT, true>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
+    else SD_LAUNCH((k_stats<DT, false>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
+    return SD_OK;
+}
+
+int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, int slot_cnt, void* stream) {
+    if (slot_cnt <= 0) return SD_OK;
+    if (dt == SD_BF16) return launch_stats_dt<SD_BF16>(P, fast, slot_lo, slot_cnt, stream);
+    if (dt == SD_F32) return launch_stats_dt<SD_F32>(P, fast, slot_lo, slot_cnt, stream);
+    return launch_stats_dt<SD_F16>(P, fast, slot_lo, slot_cnt, stream);
+}
+
+template <int TDT, int DDT>
+int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
+    const dim3 grid(P.rn_chunks, P.B);
+    if (P.noise.mode == SD_NOISE_STREAM) SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_STREAM, false>), grid, dim3(kThreads), stream, P);
+    else SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_PHILOX, true>), grid, dim3(kThreads), stream, P);
+    return SD_OK;
+}
+
+template <int TDT>
+int32_t launch_resample_t(const sd::Plan& P, int ddt, void* stream) {
+    if (ddt == SD_BF16) return launch_resample_dd<TDT, SD_BF16>(P, stream);
+    if (ddt == SD_F32) return launch_resample_dd<TDT, SD_F32>(P, stream);
+    return launch_resample_dd<TDT, SD_F16>(P, stream);
+}
+
+int32_t launch_resample(const sd::Plan& P, void* stream) {
+    const int ddt = P.draft_is_probs ? SD_F32 : P.ddt;
+    if (P.tdt == SD_BF16) return launch_resample_t<SD_BF16>(P, ddt, stream);
+    if (P.tdt == SD_F32) return launch_resample_t<SD_F32>(P, ddt, stream);
+    return launch_resample_t<SD_F16>(P, ddt, stream);
+}
+
+template <int DT>
+int32_t launch_rowsample_dt(const sd::Plan& P, void* stream) {
+    const dim3 grid(P.rn_chunks, P.B);
+    if (P.noise.mode == SD_NOISE_STREAM) SD_LAUNCH((k_rowsample<DT, SD_NOISE_STREAM>), grid, dim3(kThreads), stream, P);
+    else SD_LAUNCH((k_rowsample<DT, SD_NOISE_PHILOX>), grid, dim3(kThreads), stream, P);
+    return SD_OK;
+}
+
+int32_t launch_rowsample(const sd::Plan& P, void* stream) {
+    if (P.tdt == SD_BF16) return launch_rowsample_dt<SD_BF16>(P, stream);
+    if (P.tdt == SD_F32) return launch_rowsample_dt<SD_F32>(P, stream);
+    return launch_rowsample_dt<SD_F16>(P, stream);
+}
+
+// Row statistics for every slot: one launch when target and drafter rows share a dtype.
+int32_t launch_stats(const sd::Plan& P, void* stream) {
+    const bool t_fast = P.tT == 1.0f && !P.t_keep, d_fast = P.dT == 1.0f && !P.d_keep;
+    if (P.n_dslots == 0 || (P.tdt == P.ddt && t_fast == d_fast))
+        return launch_stats_group(P, P.tdt, t_fast, 0, P.slots, stream);
+    if (int32_t st = launch_stats_group(P, P.tdt, t_fast, 0, P.n_tslots, stream)) return st;
+    return launch_stats_group(P, P.ddt, d_fast, P.n_tslots, P.n_dslots, stream);
+}
 
 }  // namespace
 
 extern "C" {
 
 int32_t sd_abi_version(void) { return SD_ABI_VERSION; }
+
+const char* sd_last_hip_error(void) { return hipGetErrorString(g_last_error); }
 
 const char* sd_status_string(int32_t s) {
     switch (s) {
@@ -783,6 +997,7 @@ size_t sd_verify_workspace_size(int32_t batch, int32_t gamma, int32_t vocab) {
 }
 
 int32_t sd_verify(const sd_verify_args* a, void* stream) {
+    clear_stale_error();
     if (!a || a->batch <= 0 || a->gamma <= 0 || a->gamma > SD_MAX_GAMMA || a->vocab <= 0) return SD_ERR_INVALID;
     if (a->rule != SD_RULE_SPEC && a->rule != SD_RULE_ENGINE) return SD_ERR_INVALID;
     if (!valid_dtype(a->target_dtype) || (!a->draft_is_probs && !valid_dtype(a->draft_dtype))) return SD_ERR_INVALID;
@@ -824,9 +1039,7 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.finished = a->finished; P.accepted_count = a->accepted_count;
 
     const int rows = P.B * P.slots;
-    const int ept = choose_ept(rows, P.V);
-    P.chunk = kThreads * ept;
-    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    set_stats_chunks(P, rows);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->batch * (2 * a->gamma + 1), a->batch, a->gamma, a->vocab);
 
@@ -834,12 +1047,15 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         const int32_t st = launch_threshold(P, a->target_proc, a->draft_proc, stream);
         if (st != SD_OK) return st;
     }
-    if (ept == kEptLarge) SD_LAUNCH(k_stats<kEptLarge>, dim3(P.n_chunks, rows), dim3(kThreads), stream, P);
-    else SD_LAUNCH(k_stats<kEptSmall>, dim3(P.n_chunks, rows), dim3(kThreads), stream, P);
-    SD_LAUNCH(k_decide, dim3(P.B), dim3(64), stream, P);
-    SD_LAUNCH(k_walk, dim3(1), dim3(256), stream, P);
-    if (ept == kEptLarge) SD_LAUNCH(k_resample<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-    else SD_LAUNCH(k_resample<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
+    set_rchunks(P);
+    if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
+    if (int32_t st = launch_stats(P, stream)) return st;
+    if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
+    if (P.noise.mode == SD_NOISE_STREAM) {   // parity mode: the reference's serial noise order
+        SD_LAUNCH(k_decide, dim3(P.B), dim3(256), stream, P);
+        SD_LAUNCH(k_walk, dim3(1), dim3(256), stream, P);
+    }
+    if (int32_t st = launch_resample(P, stream)) return st;
     SD_LAUNCH(k_finalize, dim3(P.B), dim3(64), stream, P);
     return SD_OK;
 }
@@ -853,6 +1069,7 @@ size_t sd_sample_workspace_size(int32_t rows, int32_t vocab) {
 }
 
 int32_t sd_sample(const sd_sample_args* a, void* stream) {
+    clear_stale_error();
     if (!a || a->rows <= 0 || a->vocab <= 0 || !a->logits || !a->tokens) return SD_ERR_INVALID;
     if (!valid_dtype(a->dtype) || !valid_proc(a->proc) || !(a->proc.temperature > 0.f)) return SD_ERR_INVALID;
     if (a->noise.mode == SD_NOISE_STREAM && a->proc.kind != SD_PROC_GREEDY && !a->noise.words) return SD_ERR_INVALID;
@@ -867,22 +1084,16 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     P.noise = a->noise;
     P.next_token = a->tokens; P.next_token_stride = a->tokens_stride;
     P.token_prob = a->token_prob; P.row_status = a->row_status; P.words_used = a->words_used;
-    const int ept = choose_ept(P.B, P.V);
-    P.chunk = kThreads * ept;
-    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);
     if (P.t_keep) {
         const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
         if (st != SD_OK) return st;
     }
-    if (ept == kEptLarge) {
-        SD_LAUNCH(k_stats<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-        SD_LAUNCH(k_rowsample<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-    } else {
-        SD_LAUNCH(k_stats<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-        SD_LAUNCH(k_rowsample<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-    }
+    set_rchunks(P);
+    if (int32_t st = launch_stats(P, stream)) return st;
+    if (int32_t st = launch_rowsample(P, stream)) return st;
     SD_LAUNCH(k_sample_finalize, dim3(P.B), dim3(64), stream, P);
     return SD_OK;
 }
@@ -890,6 +1101,7 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
 size_t sd_probs_workspace_size(int32_t rows, int32_t vocab) { return sd_sample_workspace_size(rows, vocab); }
 
 int32_t sd_probs(const sd_probs_args* a, void* stream) {
+    clear_stale_error();
     if (!a || a->rows <= 0 || a->vocab <= 0 || !a->logits || !a->probs) return SD_ERR_INVALID;
     if (!valid_dtype(a->dtype) || !valid_proc(a->proc) || !(a->proc.temperature > 0.f)) return SD_ERR_INVALID;
     if (a->workspace_bytes < sd_probs_workspace_size(a->rows, a->vocab) || !a->workspace) return SD_ERR_WORKSPACE;
@@ -900,22 +1112,19 @@ int32_t sd_probs(const sd_probs_args* a, void* stream) {
     P.t_keep = needs_keep(a->proc);
     P.tT = a->proc.temperature; P.dT = 1.f;
     P.trow[0] = a->logits; P.tstride = a->stride_r;
-    const int ept = choose_ept(P.B, P.V);
-    P.chunk = kThreads * ept;
-    P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);
     if (P.t_keep) {
         const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
         if (st != SD_OK) return st;
     }
-    if (ept == kEptLarge) {
-        SD_LAUNCH(k_stats<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-        SD_LAUNCH(k_writeprobs<kEptLarge>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
-    } else {
-        SD_LAUNCH(k_stats<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P);
-        SD_LAUNCH(k_writeprobs<kEptSmall>, dim3(P.n_chunks, P.B), dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
-    }
+    set_rchunks(P);
+    if (int32_t st = launch_stats(P, stream)) return st;
+    const dim3 wg(P.rn_chunks, P.B);
+    if (P.tdt == SD_BF16) SD_LAUNCH(k_writeprobs<SD_BF16>, wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    else if (P.tdt == SD_F32) SD_LAUNCH(k_writeprobs<SD_F32>, wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    else SD_LAUNCH(k_writeprobs<SD_F16>, wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
     return SD_OK;
 }
 

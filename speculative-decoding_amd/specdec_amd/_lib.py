@@ -30,7 +30,7 @@ SD_ROW_NUCLEUS_INEXACT = 0x100
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspecdec.so")
 
-EXPORTS = ("sd_abi_version", "sd_status_string", "sd_verify_workspace_size", "sd_verify",
+EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify_workspace_size", "sd_verify",
            "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",
            "sd_mt19937_fill", "sd_mt19937_advance")
 
@@ -62,6 +62,7 @@ class sd_verify_args(C.Structure):
         ("generated", C.c_void_p), ("generated_stride_b", C.c_int64), ("step", C.c_int32),
         ("finished", C.c_void_p), ("accepted_count", C.c_void_p),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+        ("prof_stats_begin", C.c_void_p), ("prof_stats_end", C.c_void_p),
     ]
 
 
@@ -83,7 +84,21 @@ class sd_probs_args(C.Structure):
     ]
 
 
+def _share_torch_hip_runtime():
+    """Load PyTorch-ROCm's bundled HIP runtime first, so libspecdec.so (NEEDED libamdhip64.so.7,
+    which that copy's SONAME satisfies) binds to the SAME runtime torch uses instead of loading
+    /opt/rocm's second copy (two runtimes in one process do not share devices or streams)."""
+    try:
+        import torch
+    except ImportError:
+        return
+    path = os.path.join(os.path.dirname(torch.__file__), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        C.CDLL(path, mode=C.RTLD_GLOBAL)
+
+
 def _load():
+    _share_torch_hip_runtime()
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"specdec_amd: {LIB_PATH} not found — build it with "
                           f"`make -C speculative-decoding_amd` (hipcc, gfx950)")
@@ -94,6 +109,7 @@ def _load():
     lib.sd_abi_version.restype = C.c_int32
     lib.sd_status_string.restype = C.c_char_p
     lib.sd_status_string.argtypes = [C.c_int32]
+    lib.sd_last_hip_error.restype = C.c_char_p
     for ws in ("sd_verify_workspace_size",):
         getattr(lib, ws).restype = C.c_size_t
         getattr(lib, ws).argtypes = [C.c_int32, C.c_int32, C.c_int32]
@@ -124,4 +140,7 @@ class SpecdecError(RuntimeError):
 
 def check(status: int, what: str):
     if status != SD_OK:
-        raise SpecdecError(f"{what}: {lib.sd_status_string(status).decode()} ({status})")
+        msg = f"{what}: {lib.sd_status_string(status).decode()} ({status})"
+        if status == SD_ERR_LAUNCH:
+            msg += f": {lib.sd_last_hip_error().decode()}"
+        raise SpecdecError(msg)

@@ -161,7 +161,7 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
            rule: int, target_proc, draft_proc, noise, stop_tokens: Optional[torch.Tensor] = None,
            skip_sample_adjustment: bool = False, draft_is_probs: bool = False,
            active: Optional[torch.Tensor] = None, engine_state: Optional[dict] = None,
-           sync_noise: bool = True) -> VerifyOut:
+           sync_noise: bool = True, prof_events=None) -> VerifyOut:
     """One verify step for B sequences.
 
     target_rows: γ+1 (SPEC) or γ (ENGINE) tensors [B, V] — row t of every sequence;
@@ -203,10 +203,11 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         raise ValueError("active must be uint8/bool [B]")
 
     i32 = dict(dtype=torch.int32, device=dev)
+    # every output is written by the kernels (no fill launches)
     out = VerifyOut(torch.empty(B, **i32), torch.empty(B, dtype=torch.long, device=dev),
-                    torch.empty(B, dtype=torch.float32, device=dev), torch.zeros(B, **i32),
-                    torch.zeros(B, **i32), torch.empty(B, **i32), torch.empty(B, **i32),
-                    torch.zeros(1, dtype=torch.long, device=dev))
+                    torch.empty(B, dtype=torch.float32, device=dev), torch.empty(B, **i32),
+                    torch.empty(B, **i32), torch.empty(B, **i32), torch.empty(B, **i32),
+                    torch.empty(1, dtype=torch.long, device=dev))
     stochastic = rule == _lib.SD_RULE_ENGINE or tspec.stochastic
     need = B * (gamma + (2 * V if stochastic else 0))
     nz, keep = _noise_struct(noise, need, dev)
@@ -243,6 +244,8 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         a.generated, a.generated_stride_b, a.step = gen.data_ptr(), gen.stride(0), int(engine_state["step"])
         a.finished, a.accepted_count = fin.data_ptr(), acc.data_ptr()
     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    if prof_events is not None:   # (torch.cuda.Event, torch.cuda.Event) around the row-stats kernel
+        a.prof_stats_begin, a.prof_stats_end = prof_events[0].cuda_event, prof_events[1].cuda_event
     _lib.check(lib.sd_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_verify")
     if isinstance(noise, StreamNoise) and sync_noise:
         noise.advance(int(out.words_used.item()))

@@ -41,7 +41,7 @@ int main(void) {
   printf("sd_noise %zu\n", sizeof(sd_noise));
   F(sd_verify_args, draft_rows) F(sd_verify_args, draft_tokens) F(sd_verify_args, target_proc)
   F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
-  F(sd_verify_args, step) F(sd_verify_args, workspace_bytes)
+  F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end)
   F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes)
   F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes)
   return 0;
