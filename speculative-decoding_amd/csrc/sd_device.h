@@ -124,6 +124,43 @@ __device__ __forceinline__ float sd_exp(float x) {
     return fmaf(r, err * 0.693147180559945309f, r);
 }
 
+// round_dt(num / den) with inv_den = 1/den.  bf16: the product num*inv_den is within ~2 fp32 ulp
+// of the true quotient, so it rounds to the same bf16 unless its low 16 bits sit within a few
+// units of the round-to-nearest-even tie (0x8000); only then is the IEEE division done.
+template <int DT>
+__device__ __forceinline__ float div_round(float num, float den, float inv_den) {
+    if constexpr (DT == SD_BF16) {
+        const float q = num * inv_den;
+        const uint32_t low = __float_as_uint(q) & 0xffffu;
+        if (low - 0x7ff0u > 0x20u) return round_bf16(q);
+        return round_bf16(num / den);
+    } else {
+        return round_dt<DT>(num / den);
+    }
+}
+
+// Probability p = round_dt(exp(y - m) / S), bit-exact, cheap for bf16: e' = exp2((y - m)*log2e)
+// (v_exp_f32 on a once-rounded argument) is within ~48 fp32 ulp of exp(y - m) for arguments above
+// -126 (no denormal results), so e'*invS rounds to the same bf16 unless its low 16 bits sit
+// within 64 units of the tie; only then (and for tiny arguments) the compensated exp + IEEE
+// division run.  Arguments below -1000 (masked logits) give exactly 0.
+template <int DT>
+__device__ __forceinline__ float prob_exact(float y, float m, float S, float invS) {
+    if constexpr (DT == SD_BF16) {
+        const float t = (y - m) * 1.44269502162933349609375f;
+        if (t >= -126.f) {
+            const float q = __builtin_amdgcn_exp2f(t) * invS;
+            const uint32_t low = __float_as_uint(q) & 0xffffu;
+            if (low - 0x7fc0u > 0x80u) return round_bf16(q);
+        } else if (t < -1000.f) {
+            return 0.f;
+        }
+        return round_bf16(sd_exp(y - m) / S);
+    } else {
+        return round_dt<DT>(sd_exp(y - m) / S);
+    }
+}
+
 // ---------------------------------------------------------------- processors
 // Per-row keep predicate produced by the top-k / nucleus threshold search:
 // kept(j) <=> x_j > tau || (x_j == tau && j <= tie_idx).   tau=-inf, tie=INT_MAX keeps all.

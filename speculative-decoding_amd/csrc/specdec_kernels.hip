@@ -51,6 +51,7 @@ struct Plan {
     int32_t B, gamma, V, rule;
     int32_t n_tslots, n_dslots, slots, n_chunks, chunk;
     int32_t rn_chunks, rchunk;   // chunking of the resample / sample passes
+    int32_t diag;                // SD_DIAG tuning bits (0 in production)
     int32_t tdt, ddt, draft_is_probs, skip_adj;
     int32_t t_keep, d_keep, t_stoch, n_stop;
     float tT, dT;
@@ -139,6 +140,7 @@ struct FSum { __device__ float operator()(float a, float b) const { return a + b
 // row, streamed through a 4-deep register pipeline (16 B per lane per stage, 16 KiB per
 // workgroup in flight) with an online rescaled sum, so loads stay in flight while exp() runs.
 constexpr int kPipe = 4;
+constexpr float kLog2e = 1.44269502162933349609375f;
 
 __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
     const float mn = fmaxf(m, m2);
@@ -153,8 +155,9 @@ __device__ __forceinline__ const void* slot_row(const Plan& P, int b, int s) {
     return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
 }
 
+// <= 80 SGPRs keeps 8 workgroups of 256 threads resident per CU (MI355X_MICROARCH.md, residency)
 template <int DT, bool FAST>
-__global__ void __launch_bounds__(kThreads) k_stats(Plan P, int slot_lo, int slot_cnt) {
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_stats(Plan P, int slot_lo, int slot_cnt) {
     __shared__ float lm[4], ls[4];
     constexpr int VEC = Elem<DT>::kVec;
     constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
@@ -171,7 +174,13 @@ __global__ void __launch_bounds__(kThreads) k_stats(Plan P, int slot_lo, int slo
     const int nit = (int)((hi - lo + STEP - 1) / STEP);
     float m = -INFINITY, acc = 0.f;
 
-    // one rescale per vector (only when its max beats the running max), one exp per element
+    // Terms are exp(y - m) = exp2((y - m) * log2e): subtract, multiply, v_exp_f32.  y - m is exact
+    // for bf16/fp16 values (and for fp32 ones within 2^24 of each other); the multiply's rounding
+    // gives each term an independent ~|y-m|*6e-8 relative error that averages down in the sum, and
+    // no rounded product is shared by all terms, so S carries no common bias.  Consumers compute
+    // numerators with the compensated sd_exp.  The running reference m may trail the true max by
+    // up to 20 (terms stay <= e^20): rescales become rare after the first vectors, and every
+    // consumer uses (m, S) as a pair.
     auto consume = [&](const float* x, int64_t e0) {
         float y[VEC];
         float vm = -INFINITY;
@@ -180,13 +189,13 @@ __global__ void __launch_bounds__(kThreads) k_stats(Plan P, int slot_lo, int slo
             y[k] = (e0 + k < hi) ? (FAST ? x[k] : process_value<DT>(x[k], e0 + k, T, has_keep, kp)) : -INFINITY;
             vm = fmaxf(vm, y[k]);
         }
-        if (vm > m) {
+        if (vm > m + 20.f) {
             acc = m > -INFINITY ? acc * sd_exp(m - vm) : 0.f;
             m = vm;
         }
         if (m > -INFINITY) {
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) acc += sd_exp(y[k] - m);
+            for (int k = 0; k < VEC; ++k) acc += __builtin_amdgcn_exp2f((y[k] - m) * kLog2e);
         }
     };
     // steady state: stages where every lane's 16-byte vector is in range.  Loads are issued
@@ -279,13 +288,82 @@ __device__ __forceinline__ float prob_dyn(int dt, const void* row, int64_t j, fl
 // global memory after a barrier could hit a line another block on this CU cached earlier.
 __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (P.n_chunks <= kWave) {
+        // one partial per lane per slot: issue every slot's load of this wave before reducing
+        constexpr int kMaxSlotsPerWave = (2 * SD_MAX_GAMMA + 1 + 3) / 4;
+        float2 v[kMaxSlotsPerWave];
+#pragma unroll
+        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
+            const int s = w + k * nw;
+            v[k] = (s < P.slots && lane < P.n_chunks) ? P.part[(int64_t)(b * P.slots + s) * P.n_chunks + lane]
+                                                      : make_float2(-INFINITY, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
+            const int s = w + k * nw;
+            if (s >= P.slots) break;
+            const float m = wave_max(v[k].x);
+            const float sum = wave_sum(v[k].x > -INFINITY ? v[k].y * sd_exp(v[k].x - m) : 0.f);
+            if (lane == 0) {
+                lstat[s] = make_float2(m, sum);
+                if (publish) P.rowstat[b * P.slots + s] = make_float2(m, sum);   // read by later launches only
+            }
+        }
+        return;
+    }
     for (int s = w; s < P.slots; s += nw) {
         const float2 ms = combine_row(P, b * P.slots + s);
         if (lane == 0) {
             lstat[s] = ms;
-            if (publish) P.rowstat[b * P.slots + s] = ms;   // read by later launches only
+            if (publish) P.rowstat[b * P.slots + s] = ms;
         }
     }
+}
+
+// Raw logits at the drafted ids (threads < γ): issued before seq_stats so both load chains overlap.
+__device__ void seq_fetch(const Plan& P, int b, float* lxt, float* lxd) {
+    if (threadIdx.x >= P.gamma) return;
+    const int i = threadIdx.x;
+    const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
+    float xt = 0.f, xd = 0.f;
+    if (tok >= 0 && tok < P.V) {
+        int dt; float T; bool keep;
+        xt = load_dyn(P.tdt, row_ptr(P, b * P.slots + i, &dt, &T, &keep), tok);
+        if (P.draft_is_probs) xd = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
+        else xd = load_dyn(P.ddt, row_ptr(P, b * P.slots + P.n_tslots + i, &dt, &T, &keep), tok);
+    }
+    lxt[i] = xt;
+    lxd[i] = xd;
+}
+
+// p(x_i), q(x_i) from the fetched raw values and the row stats (threads < γ; after a barrier)
+__device__ void seq_ratios_from(const Plan& P, int b, const float2* lstat, const float* lxt, const float* lxd,
+                                float* lp, float* lq) {
+    if (threadIdx.x >= P.gamma) return;
+    const int i = threadIdx.x;
+    const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
+    float p = 0.f, q = 0.f;
+    if (tok >= 0 && tok < P.V) {
+        const int rt = b * P.slots + i;
+        const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+        const float yt = P.tdt == SD_BF16 ? process_value<SD_BF16>(lxt[i], tok, P.tT, P.t_keep, kt)
+                       : P.tdt == SD_F32 ? process_value<SD_F32>(lxt[i], tok, P.tT, P.t_keep, kt)
+                                         : process_value<SD_F16>(lxt[i], tok, P.tT, P.t_keep, kt);
+        p = round_dyn(P.tdt, sd_exp(yt - lstat[i].x) / lstat[i].y);
+        if (P.draft_is_probs) {
+            q = lxd[i];
+        } else {
+            const int rd = b * P.slots + P.n_tslots + i;
+            const RowKeep kd = P.d_keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+            const float2 sd = lstat[P.n_tslots + i];
+            const float yd = P.ddt == SD_BF16 ? process_value<SD_BF16>(lxd[i], tok, P.dT, P.d_keep, kd)
+                           : P.ddt == SD_F32 ? process_value<SD_F32>(lxd[i], tok, P.dT, P.d_keep, kd)
+                                             : process_value<SD_F16>(lxd[i], tok, P.dT, P.d_keep, kd);
+            q = round_dyn(P.ddt, sd_exp(yd - sd.x) / sd.y);
+        }
+    }
+    lp[i] = p;
+    lq[i] = q;
 }
 
 // p(x_i), q(x_i) of the γ drafts (threads < γ; call after seq_stats + barrier)
@@ -433,7 +511,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
 // over the two rows; BONUS / PROW: argmax of the multinomial (or greedy) value of the target row.
 constexpr float kCandTol = 1.0f - 16.0f * 5.9604645e-08f;   // candidates within 16 ulp of the max
 
-template <int TDT, int DDT, int NZ, int EPT>
+template <int TDT, int DDT, int NZ, int EPT, bool FAST>
 __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float2 mst, float2 msd_in) {
     __shared__ float ldsf[8];
     __shared__ int32_t lcount;
@@ -458,6 +536,7 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
         if (P.d_keep) kd = P.keep[rd];
     }
     const bool d_al = (reinterpret_cast<uintptr_t>(drow) & 15) == 0;
+    const float t_inv = 1.0f / mst.y, d_inv = 1.0f / msd.y;
 
     float sum = 0.f, wmax = 0.f;
     float res[EPT], ev[EPT];
@@ -472,10 +551,15 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
-            const float p = round_dt<TDT>(sd_exp(process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt) - mst.x) / mst.y);
-            const float q = P.draft_is_probs
-                ? xd[k]
-                : round_dt<DDT>(sd_exp(process_value<DDT>(xd[k], j, P.dT, P.d_keep, kd) - msd.x) / msd.y);
+            const float yt = FAST ? xt[k] : process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt);
+            const float p = prob_exact<TDT>(yt, mst.x, mst.y, t_inv);
+            float q;
+            if (P.draft_is_probs) {
+                q = xd[k];
+            } else {
+                const float yd = FAST ? xd[k] : process_value<DDT>(xd[k], j, P.dT, P.d_keep, kd);
+                q = prob_exact<DDT>(yd, msd.x, msd.y, d_inv);
+            }
             const float diff = p - q;                                 // bf16/fp32 - fp32 -> fp32
             const float rr = (j < P.V && diff > 0.f) ? diff : 0.f;     // max_fn numerator, :317 clamp
             res[v * VEC + k] = rr;
@@ -517,7 +601,7 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
     }
 }
 
-template <int TDT, int NZ, int EPT>
+template <int TDT, int NZ, int EPT, bool FAST>
 __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2 mst) {
     __shared__ float ldsf[8];
     __shared__ int32_t ldsi[8];
@@ -528,6 +612,7 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
     const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const bool stoch = P.t_stoch != 0;
     const int64_t base = (int64_t)c * P.rchunk;
+    const float t_inv = 1.0f / mst.y;
     float pv = -INFINITY;
     int32_t pi = INT_MAX;
 #pragma unroll
@@ -540,8 +625,13 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = round_dt<TDT>(sd_exp(process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt) - mst.x) / mst.y);
-            const float val = stoch ? round_dt<TDT>(p / round_dt<TDT>(e[k])) : p;   // multinomial / argmax
+            const float p = prob_exact<TDT>(FAST ? xt[k] : process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt),
+                                            mst.x, mst.y, t_inv);
+            float val = p;
+            if (stoch) {   // multinomial: round_dt(p / round_dt(E))
+                const float eb = round_dt<TDT>(e[k]);
+                val = div_round<TDT>(p, eb, __builtin_amdgcn_rcpf(eb));
+            }
             if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
         }
     }
@@ -557,18 +647,31 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
 // stats from the k_stats partials, p(x_i)/q(x_i), the accept walk on Philox uniforms — which is
 // cheap next to a kernel boundary; chunk 0 publishes it for k_finalize.  STREAM (parity) mode
 // reads the decision of the serial k_decide -> k_walk stages instead.
-template <int TDT, int DDT, int NZ, bool FUSED>
-__global__ void __launch_bounds__(kThreads) k_resample(Plan P) {
+template <int TDT, int DDT, int NZ, bool FUSED, int EPT, bool FAST>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_resample(Plan P) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
     __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
     __shared__ Decision ldec;
     const int b = blockIdx.y, c = blockIdx.x;
     Decision d;
     float2 mst, msd = make_float2(0.f, 1.f);
+    if (P.diag & 1) {   // diagnostic: decision = residual at slot 0, stats from the previous call
+        d = Decision{};
+        d.mode = kModeResid;
+        d.slot = 0;
+        d.status = SD_ROW_DONE | SD_ROW_RESIDUAL;
+        mst = P.rowstat[b * P.slots];
+        msd = P.rowstat[b * P.slots + P.n_tslots];
+        if (P.diag & 2) return;
+        resid_body<TDT, DDT, NZ, EPT, FAST>(P, d, b, c, mst, msd);
+        return;
+    }
     if constexpr (FUSED) {
-        seq_stats(P, b, lstat, c == 0);
+        __shared__ float lxt[SD_MAX_GAMMA], lxd[SD_MAX_GAMMA];
+        seq_fetch(P, b, lxt, lxd);          // threads < γ: drafted ids -> raw logits (2 dependent loads)
+        seq_stats(P, b, lstat, c == 0);     // meanwhile every wave reduces k_stats partials
         __syncthreads();
-        seq_ratios(P, b, lstat, lp, lq);
+        seq_ratios_from(P, b, lstat, lxt, lxd, lp, lq);
         __syncthreads();
         if (threadIdx.x == 0) {
             int64_t used;
@@ -580,7 +683,7 @@ __global__ void __launch_bounds__(kThreads) k_resample(Plan P) {
         }
         __syncthreads();
         d = ldec;
-        if (d.mode == kModeNone) return;
+        if (d.mode == kModeNone || (P.diag & 2)) return;
         mst = lstat[d.slot];
         if (d.mode == kModeResid && !P.draft_is_probs) msd = lstat[P.n_tslots + d.slot];
     } else {
@@ -589,8 +692,8 @@ __global__ void __launch_bounds__(kThreads) k_resample(Plan P) {
         mst = P.rowstat[b * P.slots + d.slot];
         if (d.mode == kModeResid && !P.draft_is_probs) msd = P.rowstat[b * P.slots + P.n_tslots + d.slot];
     }
-    if (d.mode == kModeResid) resid_body<TDT, DDT, NZ, 8>(P, d, b, c, mst, msd);
-    else prow_body<TDT, NZ, 8>(P, d, b, c, mst);
+    if (d.mode == kModeResid) resid_body<TDT, DDT, NZ, EPT, FAST>(P, d, b, c, mst, msd);
+    else prow_body<TDT, NZ, EPT, FAST>(P, d, b, c, mst);
 }
 
 // ------------------------------------------------------------------ k_finalize
@@ -735,6 +838,7 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
     const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const int64_t base = (int64_t)c * P.rchunk;
     const int64_t woff = 2ll * P.V * r;
+    const float inv_s = 1.0f / ms.y;
     float pv = -INFINITY;
     int32_t pi = INT_MAX;
 #pragma unroll
@@ -747,8 +851,12 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = round_dt<DT>(sd_exp(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
-            const float val = P.t_stoch ? round_dt<DT>(p / round_dt<DT>(e[k])) : p;
+            const float p = prob_exact<DT>(process_value<DT>(x[k], j, P.tT, P.t_keep, kp), ms.x, ms.y, inv_s);
+            float val = p;
+            if (P.t_stoch) {
+                const float eb = round_dt<DT>(e[k]);
+                val = div_round<DT>(p, eb, __builtin_amdgcn_rcpf(eb));
+            }
             if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
         }
     }
@@ -760,9 +868,9 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
     }
 }
 
-template <int DT, int NZ>
+template <int DT, int NZ, int EPT>
 __global__ void __launch_bounds__(kThreads) k_rowsample(Plan P) {
-    rowsample_body<DT, NZ, 8>(P, blockIdx.y, blockIdx.x);
+    rowsample_body<DT, NZ, EPT>(P, blockIdx.y, blockIdx.x);
 }
 
 __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
@@ -824,9 +932,9 @@ __device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r
     }
 }
 
-template <int DT>
+template <int DT, int EPT>
 __global__ void __launch_bounds__(kThreads) k_writeprobs(Plan P, void* out, int64_t ostride) {
-    writeprobs_body<DT, 8>(P, out, ostride, blockIdx.y, blockIdx.x);
+    writeprobs_body<DT, EPT>(P, out, ostride, blockIdx.y, blockIdx.x);
 }
 
 }  // namespace sd
@@ -892,8 +1000,13 @@ void set_stats_chunks(sd::Plan& P, int rows) {
     P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
 }
 
+// Resample / sample passes: 1 or 2 stages of 2048 elements per workgroup, about 1024 workgroups so
+// the whole grid is resident at once (these kernels carry more SGPRs, so fewer blocks fit per CU).
 void set_rchunks(sd::Plan& P) {
-    P.rchunk = kThreads * kEptSmall;
+    const int64_t stage = kThreads * kEptSmall;
+    int64_t per_wg = ((int64_t)P.B * ((P.V + stage - 1) / stage) + 1023) / 1024;
+    per_wg = 1;   // measured: 2 stages (116 VGPRs, 4 waves/SIMD) ran 1.8x slower than 1 stage at 8
+    P.rchunk = (int32_t)(per_wg * stage);
     P.rn_chunks = (P.V + P.rchunk - 1) / P.rchunk;
 }
 
@@ -927,8 +1040,15 @@ int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, in
 template <int TDT, int DDT>
 int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
     const dim3 grid(P.rn_chunks, P.B);
-    if (P.noise.mode == SD_NOISE_STREAM) SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_STREAM, false>), grid, dim3(kThreads), stream, P);
-    else SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_PHILOX, true>), grid, dim3(kThreads), stream, P);
+    // FAST: T == 1 and no top-k / nucleus mask on either side (the engine rule, plain softmax)
+    const bool fast = P.tT == 1.0f && P.dT == 1.0f && !P.t_keep && !P.d_keep;
+    if (P.noise.mode == SD_NOISE_STREAM) {
+        if (fast) SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_STREAM, false, 8, true>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_STREAM, false, 8, false>), grid, dim3(kThreads), stream, P);
+    } else {
+        if (fast) SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_PHILOX, true, 8, true>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_PHILOX, true, 8, false>), grid, dim3(kThreads), stream, P);
+    }
     return SD_OK;
 }
 
@@ -949,8 +1069,8 @@ int32_t launch_resample(const sd::Plan& P, void* stream) {
 template <int DT>
 int32_t launch_rowsample_dt(const sd::Plan& P, void* stream) {
     const dim3 grid(P.rn_chunks, P.B);
-    if (P.noise.mode == SD_NOISE_STREAM) SD_LAUNCH((k_rowsample<DT, SD_NOISE_STREAM>), grid, dim3(kThreads), stream, P);
-    else SD_LAUNCH((k_rowsample<DT, SD_NOISE_PHILOX>), grid, dim3(kThreads), stream, P);
+    if (P.noise.mode == SD_NOISE_STREAM) SD_LAUNCH((k_rowsample<DT, SD_NOISE_STREAM, 8>), grid, dim3(kThreads), stream, P);
+    else SD_LAUNCH((k_rowsample<DT, SD_NOISE_PHILOX, 8>), grid, dim3(kThreads), stream, P);
     return SD_OK;
 }
 
@@ -1048,6 +1168,7 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         if (st != SD_OK) return st;
     }
     set_rchunks(P);
+    if (const char* e = getenv("SD_DIAG")) P.diag = atoi(e);
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
     if (int32_t st = launch_stats(P, stream)) return st;
     if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
@@ -1121,10 +1242,12 @@ int32_t sd_probs(const sd_probs_args* a, void* stream) {
     }
     set_rchunks(P);
     if (int32_t st = launch_stats(P, stream)) return st;
+    P.rchunk = kThreads * kEptSmall;   // plain streaming write: one stage per workgroup
+    P.rn_chunks = (P.V + P.rchunk - 1) / P.rchunk;
     const dim3 wg(P.rn_chunks, P.B);
-    if (P.tdt == SD_BF16) SD_LAUNCH(k_writeprobs<SD_BF16>, wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
-    else if (P.tdt == SD_F32) SD_LAUNCH(k_writeprobs<SD_F32>, wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
-    else SD_LAUNCH(k_writeprobs<SD_F16>, wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    if (P.tdt == SD_BF16) SD_LAUNCH((k_writeprobs<SD_BF16, 8>), wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    else if (P.tdt == SD_F32) SD_LAUNCH((k_writeprobs<SD_F32, 8>), wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
+    else SD_LAUNCH((k_writeprobs<SD_F16, 8>), wg, dim3(kThreads), stream, P, a->probs, a->probs_stride_r);
     return SD_OK;
 }
 
