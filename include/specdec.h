@@ -198,6 +198,16 @@ int32_t sd_abi_version(void);
 const char* sd_status_string(int32_t status);
 const char* sd_last_hip_error(void);   /* hipGetErrorString of the last failed launch (this thread) */
 
+/* Workspaces: device memory of at least sd_*_workspace_size bytes, ZERO-FILLED ONCE when
+ * allocated (hipMemset).  Its first block holds per-sequence arrival counters that the PHILOX
+ * verify path uses to run each sequence's decision / sampling in the last workgroup to finish;
+ * every call leaves them at zero again, so one workspace can serve any sequence of
+ * sd_verify / sd_sample / sd_probs calls on one stream (not concurrent calls).
+ * PHILOX verify supports batch <= 16384 per call (SD_ERR_UNSUPPORTED beyond).
+ *
+ * PHILOX sampling draws the residual / bonus / p-row token by inverse CDF on one Philox U[0,1)
+ * (53 bits) per row: distributionally the reference's multinomial, not its bit stream.  Greedy
+ * rows are bit-exact in both noise modes; STREAM mode reproduces torch's CPU draws exactly.  */
 size_t sd_verify_workspace_size(int32_t batch, int32_t gamma, int32_t vocab);
 int32_t sd_verify(const sd_verify_args* args, void* stream);
 

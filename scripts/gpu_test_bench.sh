@@ -1,7 +1,9 @@
 #!/bin/bash
-# GPU-box recipe: parity tests, then bench + rocprofv3 kernel-trace summary (outputs under gpurun_out/)
+# GPU-box recipe: parity + perf-mode tests, then bench + rocprofv3 kernel-trace summary
+# (outputs under gpurun_out/)
 set -eo pipefail
 cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -m pytest tests/test_gpu_perfmode.py -q -m gpu -x -s > gpurun_out/gpu_perf_tests.log 2>&1
 timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 export TMPDIR=/tmp

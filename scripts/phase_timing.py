@@ -1,0 +1,75 @@
+"""Per-workgroup phase timing of one perf-mode verify step (diagnostic; GPU box).
+
+Loads the SD_PHASE_TIMING build (make -C speculative-decoding_amd timing), runs the bench
+shape (engine rule, B=32, γ=4, V=128256 bf16, Philox) and prints, per kernel, when workgroups
+start / reach each phase relative to the kernel's first start (µs, s_memrealtime = 100 MHz).
+"""
+import os
+import sys
+
+os.environ["SPECDEC_LIB"] = "libspecdec_ts.so"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "speculative-decoding_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from specdec_amd import _lib, ops  # noqa: E402
+from specdec_amd.noise import PhiloxNoise  # noqa: E402
+
+B, G, V = 32, 4, 128256
+dev = torch.device("cuda")
+g = torch.Generator(device=dev).manual_seed(0)
+tl = (torch.randn(B, G, V, device=dev, generator=g) * 3).to(torch.bfloat16)
+dl = (tl.float() + torch.randn(B, G, V, device=dev, generator=g)).to(torch.bfloat16)
+ids = dl.float().argmax(-1)
+noise = PhiloxNoise(seed=1)
+ts = torch.zeros(16384 * 16, dtype=torch.int64, device=dev)
+
+
+def step():
+    return ops.verify([tl[:, t] for t in range(G)], [dl[:, t] for t in range(G)], ids, _lib.SD_RULE_ENGINE,
+                      ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise, torch.tensor([], dtype=torch.long, device=dev))
+
+
+for _ in range(20):
+    step()
+torch.cuda.synchronize()
+os.environ["SD_TS_PTR"] = str(ts.data_ptr())
+warm = torch.randn(8192, 8192, device=dev)
+for rep in range(3):
+    ts.zero_()
+    torch.cuda.synchronize()
+    if rep == 2:   # keep the GPU busy right up to the step (no idle gap before it)
+        for _ in range(20):
+            warm = warm @ warm
+            warm = warm / warm.norm()
+    step()
+    torch.cuda.synchronize()
+    t = ts.view(-1, 16).cpu().numpy().astype(np.int64)
+    print(f"--- rep {rep}")
+    for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "loop_end", "arrived", "decided"]),
+                                 ("k_sample_finish", 16384 - 64, 16384, ["start", "prologue", "body_end", "arrived",
+                                                            "tail_S", "cdf_pick", "finalized", "cdf_select",
+                                                            "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"]),
+                                 ("k_sample", 8192, 16384 - 64, ["start", "prologue", "body_end", "arrived",
+                                                            "tail_S", "cdf_pick", "finalized", "cdf_select",
+                                                            "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"])):
+        blk = t[lo:hi]
+        blk = blk[blk[:, 0] > 0]
+        if not len(blk):
+            continue
+        t0 = blk[:, 0].min()
+        print(f"{name}: {len(blk)} workgroups")
+        for k, ph in enumerate(phases):
+            v = blk[:, k]
+            v = v[v > 0]
+            if len(v):
+                d = (v - t0) / 100.0
+                print(f"  {ph:10s} n={len(v):5d}  min {d.min():7.2f}  p50 {np.median(d):7.2f}  max {d.max():7.2f} us")
+    blk = t[8192:16384]
+    sel = (blk[:, 4] > 0) & (blk[:, 10] > 0)
+    if sel.any():
+        real = (blk[sel, 10] - blk[sel, 4]).astype(np.float64)       # 100 MHz ticks
+        core = (blk[sel, 13] - blk[sel, 12]).astype(np.float64)      # shader clock ticks
+        print(f"  tail shader clock: {np.median(core / real) * 100:.0f} MHz (median over {sel.sum()} tails)")

@@ -10,6 +10,7 @@
 #include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <climits>
 
 #include "specdec.h"
 
@@ -110,6 +111,84 @@ __device__ __forceinline__ void load_vec(const void* row, int64_t e0, int vocab,
     }
 }
 
+// Load N consecutive elements starting at e0 (N a divisor of kVec, e0 a multiple of N): one
+// 16-, 8- or 4-byte vector when the row is 16-byte aligned and in range, else guarded scalars.
+// Mixed-width pairs (bf16 target with fp32 drafter) step both rows by the narrower vector.
+template <int DT, int N>
+__device__ __forceinline__ void load_vecn(const void* row, int64_t e0, int vocab, bool aligned, float* out) {
+    static_assert(Elem<DT>::kVec % N == 0, "N must divide the 16-byte vector");
+    if constexpr (N == Elem<DT>::kVec) {
+        load_vec<DT>(row, e0, vocab, aligned, out);
+    } else {
+        constexpr int kB = N * Elem<DT>::kBytes;
+        if (aligned && e0 + N <= vocab) {
+            const char* a = static_cast<const char*>(row) + e0 * Elem<DT>::kBytes;
+            uint32_t ws[4];
+            if constexpr (kB == 8) {
+                const uint2 w = *reinterpret_cast<const uint2*>(a);
+                ws[0] = w.x; ws[1] = w.y;
+            } else {
+                static_assert(kB == 4, "unsupported width");
+                ws[0] = *reinterpret_cast<const uint32_t*>(a);
+            }
+#pragma unroll
+            for (int k = 0; k < kB / 4; ++k) {
+                if constexpr (DT == SD_F32) {
+                    out[k] = __uint_as_float(ws[k]);
+                } else if constexpr (DT == SD_BF16) {
+                    out[2 * k] = __uint_as_float(ws[k] << 16);
+                    out[2 * k + 1] = __uint_as_float(ws[k] & 0xffff0000u);
+                } else {
+                    out[2 * k] = __half2float(__ushort_as_half((unsigned short)(ws[k] & 0xffffu)));
+                    out[2 * k + 1] = __half2float(__ushort_as_half((unsigned short)(ws[k] >> 16)));
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < N; ++k) out[k] = (e0 + k < vocab) ? load_one<DT>(row, e0 + k) : 0.f;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- cross-workgroup exchange
+// Data handed between workgroups of ONE kernel (the last-arrival tails) goes through
+// agent-coherent stores / loads (relaxed agent-scope atomics: `sc1` on gfx950, write-through /
+// bypass of the per-XCD L2 for these few words) instead of an agent-scope release / acquire,
+// which on gfx950 is a whole-L2 writeback + invalidate (buffer_wbl2 / buffer_inv) per workgroup.
+__device__ __forceinline__ void st_coh(float* p, float v) {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(int32_t* p, int32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(float2* p, float2 v) {
+    const uint64_t u = ((uint64_t)__float_as_uint(v.y) << 32) | __float_as_uint(v.x);
+    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_coh(const float* p) {
+    return __uint_as_float(__hip_atomic_load(reinterpret_cast<uint32_t*>(const_cast<float*>(p)), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ int32_t ld_coh(const int32_t* p) {
+    return __hip_atomic_load(const_cast<int32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float2 ld_coh(const float2* p) {
+    const uint64_t u = __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<float2*>(p)), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return make_float2(__uint_as_float((uint32_t)u), __uint_as_float((uint32_t)(u >> 32)));
+}
+// coherent only when another workgroup of the SAME launch may have written p (last-arrival tails);
+// data from an earlier launch is read with plain (cacheable) loads
+template <typename T>
+__device__ __forceinline__ T ld_x(const T* p, bool coh) { return coh ? ld_coh(p) : *p; }
+
+// this wave's coherent stores have completed (s_waitcnt 0), and the compiler keeps order
+__device__ __forceinline__ void coh_wait() {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_waitcnt(0);
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+}
+
 // ---------------------------------------------------------------- exp
 // e^x with v_exp_f32 (2^t) and the rounding error of t = x*log2(e) folded back in by FMA:
 // ~1 ulp like ocml's expf but without its range/denormal branches.  Every kernel uses this
@@ -187,21 +266,96 @@ __device__ __forceinline__ float process_value(float x, int64_t j, float T, bool
     return v;
 }
 
-// ---------------------------------------------------------------- reductions
+// ---------------------------------------------------------------- wave primitives (DPP)
+// Cross-lane steps use DPP lane shuffles (a VALU operand modifier, a few cycles) instead of
+// __shfl (ds_bpermute through the LDS crossbar, ~100 cycles per dependent step).  Reductions:
+// quad_perm x2, row_half_mirror, row_mirror (every lane holds its row's result), then
+// row_bcast15 / row_bcast31 fold rows 0..3 into lane 63, broadcast with readlane.  Scans:
+// row_shr 1,2,4,8 (Hillis-Steele inside each 16-lane row), then row_bcast15 / row_bcast31.
+// The combining order is fixed, so results are deterministic.  Call with all 64 lanes active.
+enum : int {
+    kDppQuad1032 = 0xB1, kDppQuad2301 = 0x4E, kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114,
+    kDppRowShr8 = 0x118, kDppRowMirror = 0x140, kDppRowHalfMirror = 0x141, kDppRowBcast15 = 0x142,
+    kDppRowBcast31 = 0x143
+};
+
+template <int CTRL, int ROWS = 0xF, bool BOUND0 = false>
+__device__ __forceinline__ int dpp_i(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWS, 0xF, BOUND0);
+}
+template <int CTRL, int ROWS = 0xF, bool BOUND0 = false>
+__device__ __forceinline__ float dpp_f(float old, float v) {
+    return __int_as_float(dpp_i<CTRL, ROWS, BOUND0>(__float_as_int(old), __float_as_int(v)));
+}
+template <int CTRL, int ROWS = 0xF, bool BOUND0 = false>
+__device__ __forceinline__ double dpp_d(double old, double v) {
+    const uint64_t o = __double_as_longlong(old), x = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)dpp_i<CTRL, ROWS, BOUND0>((int)(uint32_t)o, (int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)dpp_i<CTRL, ROWS, BOUND0>((int)(uint32_t)(o >> 32), (int)(uint32_t)(x >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ __forceinline__ float lane63_f(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63)); }
+__device__ __forceinline__ int lane63_i(int v) { return __builtin_amdgcn_readlane(v, 63); }
+
+// all-lanes reduction of v with op (identity id): the result is uniform across the wave
+template <typename Op>
+__device__ __forceinline__ float wave_reduce(float v, float id, Op op) {
+    v = op(v, dpp_f<kDppQuad1032>(id, v));
+    v = op(v, dpp_f<kDppQuad2301>(id, v));
+    v = op(v, dpp_f<kDppRowHalfMirror>(id, v));
+    v = op(v, dpp_f<kDppRowMirror>(id, v));
+    v = op(v, dpp_f<kDppRowBcast15, 0xA>(id, v));
+    v = op(v, dpp_f<kDppRowBcast31, 0xC>(id, v));
+    return lane63_f(v);
+}
+template <typename Op>
+__device__ __forceinline__ int wave_reduce_i(int v, int id, Op op) {
+    v = op(v, dpp_i<kDppQuad1032>(id, v));
+    v = op(v, dpp_i<kDppQuad2301>(id, v));
+    v = op(v, dpp_i<kDppRowHalfMirror>(id, v));
+    v = op(v, dpp_i<kDppRowMirror>(id, v));
+    v = op(v, dpp_i<kDppRowBcast15, 0xA>(id, v));
+    v = op(v, dpp_i<kDppRowBcast31, 0xC>(id, v));
+    return lane63_i(v);
+}
+
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
-    return v;
+    return wave_reduce(v, -INFINITY, [](float a, float b) { return fmaxf(a, b); });
 }
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+    return wave_reduce(v, 0.f, [](float a, float b) { return a + b; });
+}
+__device__ __forceinline__ int wave_min_i(int v) {
+    return wave_reduce_i(v, INT_MAX, [](int a, int b) { return a < b ? a : b; });
+}
+__device__ __forceinline__ int wave_max_i(int v) {
+    return wave_reduce_i(v, INT_MIN, [](int a, int b) { return a > b ? a : b; });
+}
+
+// inclusive prefix sums across the wave (lane order)
+__device__ __forceinline__ float wave_incl_scan(float v) {
+    v += dpp_f<kDppRowShr1, 0xF, true>(0.f, v);
+    v += dpp_f<kDppRowShr2, 0xF, true>(0.f, v);
+    v += dpp_f<kDppRowShr4, 0xF, true>(0.f, v);
+    v += dpp_f<kDppRowShr8, 0xF, true>(0.f, v);
+    v += dpp_f<kDppRowBcast15, 0xA>(0.f, v);
+    v += dpp_f<kDppRowBcast31, 0xC>(0.f, v);
     return v;
 }
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+__device__ __forceinline__ double wave_incl_scan_d(double v) {
+    v += dpp_d<kDppRowShr1, 0xF, true>(0.0, v);
+    v += dpp_d<kDppRowShr2, 0xF, true>(0.0, v);
+    v += dpp_d<kDppRowShr4, 0xF, true>(0.0, v);
+    v += dpp_d<kDppRowShr8, 0xF, true>(0.0, v);
+    v += dpp_d<kDppRowBcast15, 0xA>(0.0, v);
+    v += dpp_d<kDppRowBcast31, 0xC>(0.0, v);
     return v;
+}
+__device__ __forceinline__ double lane_d(double v, int lane) {
+    const uint64_t x = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 // torch.argmax semantics: NaN is the maximum; among equal maxima the first index wins.
@@ -211,13 +365,22 @@ __device__ __forceinline__ bool arg_better(float a, int32_t ia, float b, int32_t
     return a > b || (a == b && ia < ib);
 }
 
+// (v, i) argmax across the wave (arg_better order); the result is uniform across the wave
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ void argmax_step(float& v, int32_t& i) {
+    const float ov = dpp_f<CTRL, ROWS>(-INFINITY, v);
+    const int32_t oi = dpp_i<CTRL, ROWS>(INT_MAX, i);
+    if (arg_better(ov, oi, v, i)) { v = ov; i = oi; }
+}
 __device__ __forceinline__ void wave_argmax(float& v, int32_t& i) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(v, o, kWave);
-        const int32_t oi = __shfl_xor(i, o, kWave);
-        if (arg_better(ov, oi, v, i)) { v = ov; i = oi; }
-    }
+    argmax_step<kDppQuad1032>(v, i);
+    argmax_step<kDppQuad2301>(v, i);
+    argmax_step<kDppRowHalfMirror>(v, i);
+    argmax_step<kDppRowMirror>(v, i);
+    argmax_step<kDppRowBcast15, 0xA>(v, i);
+    argmax_step<kDppRowBcast31, 0xC>(v, i);
+    v = lane63_f(v);
+    i = lane63_i(i);
 }
 
 // ---------------------------------------------------------------- noise
@@ -244,12 +407,18 @@ __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
     return c;
 }
 
-enum PhiloxSite : uint32_t { kSiteAccept = 1, kSiteSample = 2 };
+enum PhiloxSite : uint32_t { kSiteAccept = 1, kSiteSample = 2, kSiteCdf = 3 };
 
 __device__ __forceinline__ uint4 philox_block(const sd_noise& nz, uint32_t row, uint32_t site, uint32_t idx) {
     const uint4 c = make_uint4(idx, (row & 0x00ffffffu) | (site << 24), (uint32_t)nz.offset,
                                (uint32_t)(nz.offset >> 32));
     return philox4x32_10(c, make_uint2((uint32_t)nz.seed, (uint32_t)(nz.seed >> 32)));
+}
+
+// perf-mode U[0,1) at 53 bits for one inverse-CDF draw of row `row`
+__device__ __forceinline__ double cdf_uniform(const sd_noise& nz, uint32_t row) {
+    const uint4 q = philox_block(nz, row, kSiteCdf, 0u);
+    return (double)(((((uint64_t)q.x) << 32) | q.y) >> 11) * 1.1102230246251565e-16;   // 2^-53
 }
 
 // perf-mode Exp(1) from one 32-bit word: u in (0,1) at 24 bits, E = -ln(u) in fp32

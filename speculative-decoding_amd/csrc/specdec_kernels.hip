@@ -1,18 +1,24 @@
 // specdec_kernels.hip — fused speculative verify/accept/resample for MI355X (gfx950).
 //
 // One verify step (sd_verify) is a short chain of memory-bound kernels on one stream,
-// with no host sync and no allocation:
+// with no host sync and no allocation.
 //
-//   k_threshold  (top-k / nucleus rows only) radix descent for the keep threshold   -> RowKeep
-//   k_stats      grid (chunk, row): per-chunk max / Σexp of the processed row      -> partials
-//   k_decide     grid (B): combine partials -> (M, S) per row; p(x_i), q(x_i)
-//   k_walk       accept rule walk (A8 / A10), noise offsets, per-row decision
-//   k_resample   grid (chunk, B): Σ(p_n - q_n)+ and exact argmax candidates of the
-//                residual / bonus / p-row sample, in ONE pass over the two rows
-//   k_finalize   grid (B): combine, exact candidate evaluation, outputs, engine state
+// PHILOX (perf) mode — two launches:
+//   k_stats<TAIL>   grid (span, row): per-span max / Σexp of the processed row -> partials.
+//                   The last workgroup of each sequence (agent-scope counter) then decides it:
+//                   row stats, p(x_i)/q(x_i), the accept walk -> Decision, prune lengths.
+//   k_sample        grid (chunk, B): per-chunk Σ weight of the row to sample — (p_n - q_n)+
+//                   (residual) or p (bonus / p-row) — then the last workgroup of each sequence
+//                   draws the token by inverse CDF (fp64 scan inside one chunk), writes the
+//                   outputs and applies the engine state.  Greedy rows take an exact argmax.
 //
-// Every logit row is read once by k_stats (the algorithmic bytes); k_resample re-reads
-// at most two rows per sequence (served from the 256 MiB Infinity Cache).  See DESIGN.md.
+// STREAM (parity) mode keeps the reference's serial noise order:
+//   k_stats -> k_decide (grid B) -> k_walk (serial over rows) -> k_resample (exponential race
+//   with exact candidates, torch's own words) -> k_finalize.
+//
+// k_threshold (top-k / nucleus rows only) runs first in both modes.  Every logit row is read
+// once by k_stats (the algorithmic bytes); the sampling pass re-reads at most two rows per
+// sequence (served from the 256 MiB Infinity Cache).  See DESIGN.md.
 #include <hip/hip_runtime.h>
 
 #include <climits>
@@ -51,7 +57,6 @@ struct Plan {
     int32_t B, gamma, V, rule;
     int32_t n_tslots, n_dslots, slots, n_chunks, chunk;
     int32_t rn_chunks, rchunk;   // chunking of the resample / sample passes
-    int32_t diag;                // SD_DIAG tuning bits (0 in production)
     int32_t tdt, ddt, draft_is_probs, skip_adj;
     int32_t t_keep, d_keep, t_stoch, n_stop;
     float tT, dT;
@@ -89,7 +94,40 @@ struct Plan {
     Decision* dec;
     ResPart* rpart;
     int32_t* keep_hist;   // threshold scratch
+    uint32_t* cnt;        // per-sequence arrival counters (seq_counter): set 0 k_stats, set 1 k_sample
+    uint64_t* ts;         // SD_PHASE_TIMING builds only: per-workgroup phase timestamps
+    int32_t tails;        // perf mode: decide / finish in last-arrival tails (1) or own launches (0)
+    int32_t coh;          // partials may come from the same launch: read them agent-coherently
 };
+
+// Phase timestamps (diagnostic builds, -DSD_PHASE_TIMING): thread 0 of workgroup `wg` records
+// s_memrealtime (100 MHz) at phase `ph`; k_stats workgroups at [0, 8192), k_sample at 8192+.
+#ifdef SD_PHASE_TIMING
+#define SD_TS(wg, ph)                                                                          \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && P.ts) {                                                        \
+            P.ts[(size_t)(wg) * 16 + (ph)] = __builtin_amdgcn_s_memrealtime();                 \
+            if ((ph) == 4 || (ph) == 10) P.ts[(size_t)(wg) * 16 + 12 + ((ph) == 10)] = __builtin_amdgcn_s_memtime(); \
+        }                                                                                      \
+    } while (0)
+#else
+#define SD_TS(wg, ph) \
+    do {              \
+        (void)(wg);   \
+    } while (0)
+#endif
+
+// Arrival counters live in a fixed block at the front of every workspace layout, so calls with
+// different shapes sharing one workspace never overwrite them.  They are zero between calls
+// (the last arriving workgroup resets its counter); the workspace must be zero-filled once.
+// One counter per 128-byte line: device-scope atomics execute beyond the per-XCD L2, and
+// counters sharing a line would serialise every sequence's arrivals on it.
+constexpr int kCntMax = 16384;
+constexpr int kTailChunks = 1024;   // perf-mode sampling: chunk partials staged in LDS (V <= 2 Mi)
+constexpr int kCntStride = 32;   // uint32 words per counter (128 B)
+__device__ __forceinline__ uint32_t* seq_counter(const uint32_t* base, int set, int b) {
+    return const_cast<uint32_t*>(base) + ((size_t)set * kCntMax + b) * kCntStride;
+}
 
 __device__ __forceinline__ const void* row_ptr(const Plan& P, int r, int* dt, float* T, bool* keep) {
     const int b = r / P.slots, s = r - b * P.slots;
@@ -108,16 +146,37 @@ __device__ __forceinline__ bool is_stop(const Plan& P, int64_t tok) {
 }
 
 // ------------------------------------------------------------------ block helpers
+struct FMax {
+    static constexpr float kId = -INFINITY;
+    __device__ float operator()(float a, float b) const { return fmaxf(a, b); }
+};
+struct FSum {
+    static constexpr float kId = 0.f;
+    __device__ float operator()(float a, float b) const { return a + b; }
+};
+
 template <typename F>
 __device__ __forceinline__ float block_reduce(float v, F op, float* lds) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = op(v, __shfl_xor(v, o, kWave));
+    v = wave_reduce(v, F::kId, op);
     __syncthreads();
     if (lane == 0) lds[w] = v;
     __syncthreads();
     float r = lds[0];
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = op(r, lds[k]);
+    return r;
+}
+
+// two sums at once (fixed order)
+__device__ __forceinline__ float2 block_reduce2(float2 v, float* lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    v.x = wave_sum(v.x);
+    v.y = wave_sum(v.y);
+    __syncthreads();
+    if (lane == 0) { lds[2 * w] = v.x; lds[2 * w + 1] = v.y; }
+    __syncthreads();
+    float2 r = make_float2(lds[0], lds[1]);
+    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) { r.x += lds[2 * k]; r.y += lds[2 * k + 1]; }
     return r;
 }
 
@@ -132,8 +191,6 @@ __device__ __forceinline__ void block_argmax(float& v, int32_t& i, float* ldsv, 
         if (arg_better(ldsv[k], ldsi[k], v, i)) { v = ldsv[k]; i = ldsi[k]; }
 }
 
-struct FMax { __device__ float operator()(float a, float b) const { return fmaxf(a, b); } };
-struct FSum { __device__ float operator()(float a, float b) const { return a + b; } };
 
 // ------------------------------------------------------------------ k_stats
 // grid (span, row-of-group): running max / Σexp of y = round_dt(_process(x)/T) over one span of a
@@ -149,21 +206,49 @@ __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float
     m = mn;
 }
 
+// one DPP step of the (max, rescaled sum) wave merge; rows outside ROWS merge the identity
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ void merge_step(float& m, float& s) {
+    const float m2 = dpp_f<CTRL, ROWS>(-INFINITY, m), s2 = dpp_f<CTRL, ROWS>(0.f, s);
+    online_merge(m, s, m2, s2);
+}
+
 __device__ __forceinline__ const void* slot_row(const Plan& P, int b, int s) {
     if (s < P.n_tslots)
         return static_cast<const char*>(P.trow[s]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
     return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
 }
 
+__device__ void decide_seq(const Plan& P, int b, float pf_xt, float pf_xd);
+__device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd);
+
+// Arrival at a per-sequence counter (thread 0, after storing its partials with st_coh): true for
+// the last of `total` arrivals, which also re-arms the counter.  coh_wait() completes the
+// coherent stores before the increment; the last arrival reads every partial with ld_coh.
+__device__ __forceinline__ bool arrive_last(uint32_t* ctr, uint32_t total) {
+    coh_wait();
+    const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev + 1u != total) return false;
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
 // <= 80 SGPRs keeps 8 workgroups of 256 threads resident per CU (MI355X_MICROARCH.md, residency)
-template <int DT, bool FAST>
+// TAIL (perf mode): the last workgroup to finish a sequence's rows runs its decision (decide_seq).
+template <int DT, bool FAST, bool TAIL>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_stats(Plan P, int slot_lo, int slot_cnt) {
     __shared__ float lm[4], ls[4];
     constexpr int VEC = Elem<DT>::kVec;
     constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
+    const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
+    SD_TS(wg_id, 0);
     const int b = blockIdx.y / slot_cnt, s = slot_lo + blockIdx.y % slot_cnt;
     const int r = b * P.slots + s;
     const void* row = slot_row(P, b, s);
+    // TAIL: drafted ids now (consumed after the loop), their logits right after it, so a
+    // workgroup that turns out to be its sequence's last arrival has them in registers
+    int64_t pf_tok = -1;
+    if (TAIL && threadIdx.x < P.gamma) pf_tok = P.draft_tokens[b * P.tok_stride + threadIdx.x];
     const bool is_t = s < P.n_tslots;
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
@@ -237,19 +322,35 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < hi) ? load_one<DT>(row, e0 + k) : 0.f;
         consume(x, e0);
     }
-    // workgroup combine (fixed order)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const float m2 = __shfl_xor(m, o, kWave), s2 = __shfl_xor(acc, o, kWave);
-        online_merge(m, acc, m2, s2);
-    }
+    float pf_xt = 0.f, pf_xd = 0.f;
+    if (TAIL && threadIdx.x < P.gamma) fetch_drafted(P, b, threadIdx.x, pf_tok, &pf_xt, &pf_xd);
+    // workgroup combine (fixed order): DPP wave merge, then the 4 waves through LDS
+    merge_step<kDppQuad1032>(m, acc);
+    merge_step<kDppQuad2301>(m, acc);
+    merge_step<kDppRowHalfMirror>(m, acc);
+    merge_step<kDppRowMirror>(m, acc);
+    merge_step<kDppRowBcast15, 0xA>(m, acc);
+    merge_step<kDppRowBcast31, 0xC>(m, acc);
+    m = lane63_f(m);
+    acc = lane63_f(acc);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (lane == 0) { lm[w] = m; ls[w] = acc; }
     __syncthreads();
+    SD_TS(wg_id, 1);
     if (threadIdx.x == 0) {
         float M = lm[0], S = ls[0];
         for (int k = 1; k < kThreads / kWave; ++k) online_merge(M, S, lm[k], ls[k]);
-        P.part[(int64_t)r * P.n_chunks + blockIdx.x] = make_float2(M, S);
+        st_coh(P.part + (int64_t)r * P.n_chunks + blockIdx.x, make_float2(M, S));
+    }
+    if constexpr (TAIL) {
+        __shared__ int s_last;
+        if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.slots * P.n_chunks));
+        __syncthreads();
+        SD_TS(wg_id, 2);
+        if (s_last) {
+            decide_seq(P, b, pf_xt, pf_xd);
+            SD_TS(wg_id, 3);
+        }
     }
 }
 
@@ -258,12 +359,14 @@ __device__ __forceinline__ float2 combine_row(const Plan& P, int r) {
     const int lane = threadIdx.x & 63;
     const float2* pr = P.part + (int64_t)r * P.n_chunks;
     float m = -INFINITY;
-    for (int c = lane; c < P.n_chunks; c += kWave) m = fmaxf(m, pr[c].x);
+    for (int c = lane; c < P.n_chunks; c += kWave) m = fmaxf(m, ld_x(pr + c, P.coh).x);
     m = wave_max(m);
     // fixed-order sum: lane-strided partial sums, then a fixed butterfly
     float s = 0.f;
-    for (int c = lane; c < P.n_chunks; c += kWave)
-        if (pr[c].x > -INFINITY) s += pr[c].y * sd_exp(pr[c].x - m);
+    for (int c = lane; c < P.n_chunks; c += kWave) {
+        const float2 v = ld_x(pr + c, P.coh);
+        if (v.x > -INFINITY) s += v.y * sd_exp(v.x - m);
+    }
     s = wave_sum(s);
     return make_float2(m, s);
 }
@@ -295,7 +398,7 @@ __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
 #pragma unroll
         for (int k = 0; k < kMaxSlotsPerWave; ++k) {
             const int s = w + k * nw;
-            v[k] = (s < P.slots && lane < P.n_chunks) ? P.part[(int64_t)(b * P.slots + s) * P.n_chunks + lane]
+            v[k] = (s < P.slots && lane < P.n_chunks) ? ld_x(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane, P.coh)
                                                       : make_float2(-INFINITY, 0.f);
         }
 #pragma unroll
@@ -320,20 +423,16 @@ __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
     }
 }
 
-// Raw logits at the drafted ids (threads < γ): issued before seq_stats so both load chains overlap.
-__device__ void seq_fetch(const Plan& P, int b, float* lxt, float* lxd) {
-    if (threadIdx.x >= P.gamma) return;
-    const int i = threadIdx.x;
-    const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
-    float xt = 0.f, xd = 0.f;
+// Raw target / drafter values at drafted id tok of draft i (0 for an out-of-range id).
+__device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd) {
+    *xt = 0.f;
+    *xd = 0.f;
     if (tok >= 0 && tok < P.V) {
         int dt; float T; bool keep;
-        xt = load_dyn(P.tdt, row_ptr(P, b * P.slots + i, &dt, &T, &keep), tok);
-        if (P.draft_is_probs) xd = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
-        else xd = load_dyn(P.ddt, row_ptr(P, b * P.slots + P.n_tslots + i, &dt, &T, &keep), tok);
+        *xt = load_dyn(P.tdt, row_ptr(P, b * P.slots + i, &dt, &T, &keep), tok);
+        if (P.draft_is_probs) *xd = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
+        else *xd = load_dyn(P.ddt, row_ptr(P, b * P.slots + P.n_tslots + i, &dt, &T, &keep), tok);
     }
-    lxt[i] = xt;
-    lxd[i] = xd;
 }
 
 // p(x_i), q(x_i) from the fetched raw values and the row stats (threads < γ; after a barrier)
@@ -506,6 +605,33 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
     }
 }
 
+// Perf-mode decision of sequence b by one 256-thread workgroup (the k_stats tail): row stats
+// from the partials (published to rowstat for the sampling pass), p/q at the drafted ids, the
+// accept walk on Philox uniforms.
+__device__ void decide_seq(const Plan& P, int b, float pf_xt, float pf_xd) {
+    __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
+    __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA], lxt[SD_MAX_GAMMA], lxd[SD_MAX_GAMMA];
+    if (threadIdx.x < P.gamma) { lxt[threadIdx.x] = pf_xt; lxd[threadIdx.x] = pf_xd; }   // prefetched
+    seq_stats(P, b, lstat, true);       // every wave reduces partials
+    __syncthreads();
+    seq_ratios_from(P, b, lstat, lxt, lxd, lp, lq);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t used;
+        const Decision d = walk_core(P, b, lp, lq, 0, &used);
+        publish_decision(P, b, d);
+        if (P.words_used && b == 0) *P.words_used = 0;
+    }
+}
+
+// grid (B): decide_seq as its own launch (perf mode without the k_stats tail)
+__global__ void __launch_bounds__(kThreads) k_decide_perf(Plan P) {
+    const int b = blockIdx.x;
+    float xt = 0.f, xd = 0.f;
+    if (threadIdx.x < P.gamma) fetch_drafted(P, b, threadIdx.x, P.draft_tokens[b * P.tok_stride + threadIdx.x], &xt, &xd);
+    decide_seq(P, b, xt, xd);
+}
+
 // ------------------------------------------------------------------ k_resample
 // grid (chunk, B).  RESID: Σ(p_n - q_n)+ and the argmax candidates of fl(fl(res/S)/E) in one pass
 // over the two rows; BONUS / PROW: argmax of the multinomial (or greedy) value of the target row.
@@ -544,9 +670,8 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
     for (int v = 0; v < NV; ++v) {
         const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
         float xt[VEC], xd[VEC], e[VEC];
-        load_vec<TDT>(trow, e0, P.V, t_al, xt);
-        if (P.draft_is_probs) load_vec<SD_F32>(drow, e0, P.V, d_al, xd);
-        else load_vec<DDT>(drow, e0, P.V, d_al, xd);
+        load_vecn<TDT, VEC>(trow, e0, P.V, t_al, xt);
+        load_vecn<DDT, VEC>(drow, e0, P.V, d_al, xd);   // draft_is_probs dispatches DDT = F32
         if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
@@ -594,10 +719,14 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
     __syncthreads();
     if (threadIdx.x == 0) {
         ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
-        o.sum = bsum;
-        o.wmax = bw;
-        o.ncand = lcount;
-        for (int k = 0; k < kMaxCand && k < lcount; ++k) { o.cres[k] = lres[k]; o.ce[k] = le[k]; o.cidx[k] = lidx[k]; }
+        st_coh(&o.sum, bsum);
+        st_coh(&o.wmax, bw);
+        st_coh(&o.ncand, lcount);
+        for (int k = 0; k < kMaxCand && k < lcount; ++k) {
+            st_coh(&o.cres[k], lres[k]);
+            st_coh(&o.ce[k], le[k]);
+            st_coh(&o.cidx[k], lidx[k]);
+        }
     }
 }
 
@@ -638,185 +767,474 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
     block_argmax(pv, pi, ldsf, ldsi);
     if (threadIdx.x == 0) {
         ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
-        o.pval = pv;
-        o.pidx = pi;
+        st_coh(&o.pval, pv);
+        st_coh(&o.pidx, pi);
     }
 }
 
-// FUSED (perf mode): every workgroup of sequence b first re-derives the decision itself — row
-// stats from the k_stats partials, p(x_i)/q(x_i), the accept walk on Philox uniforms — which is
-// cheap next to a kernel boundary; chunk 0 publishes it for k_finalize.  STREAM (parity) mode
-// reads the decision of the serial k_decide -> k_walk stages instead.
-template <int TDT, int DDT, int NZ, bool FUSED, int EPT, bool FAST>
+// STREAM (parity) mode: the decision comes from the serial k_decide -> k_walk stages.
+template <int TDT, int DDT, int EPT, bool FAST>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_resample(Plan P) {
-    __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
-    __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
-    __shared__ Decision ldec;
     const int b = blockIdx.y, c = blockIdx.x;
-    Decision d;
-    float2 mst, msd = make_float2(0.f, 1.f);
-    if (P.diag & 1) {   // diagnostic: decision = residual at slot 0, stats from the previous call
-        d = Decision{};
-        d.mode = kModeResid;
-        d.slot = 0;
-        d.status = SD_ROW_DONE | SD_ROW_RESIDUAL;
-        mst = P.rowstat[b * P.slots];
-        msd = P.rowstat[b * P.slots + P.n_tslots];
-        if (P.diag & 2) return;
-        resid_body<TDT, DDT, NZ, EPT, FAST>(P, d, b, c, mst, msd);
-        return;
-    }
-    if constexpr (FUSED) {
-        __shared__ float lxt[SD_MAX_GAMMA], lxd[SD_MAX_GAMMA];
-        seq_fetch(P, b, lxt, lxd);          // threads < γ: drafted ids -> raw logits (2 dependent loads)
-        seq_stats(P, b, lstat, c == 0);     // meanwhile every wave reduces k_stats partials
-        __syncthreads();
-        seq_ratios_from(P, b, lstat, lxt, lxd, lp, lq);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int64_t used;
-            ldec = walk_core(P, b, lp, lq, 0, &used);
-            if (c == 0) {
-                publish_decision(P, b, ldec);
-                if (P.words_used && b == 0) *P.words_used = 0;
-            }
-        }
-        __syncthreads();
-        d = ldec;
-        if (d.mode == kModeNone || (P.diag & 2)) return;
-        mst = lstat[d.slot];
-        if (d.mode == kModeResid && !P.draft_is_probs) msd = lstat[P.n_tslots + d.slot];
-    } else {
-        d = P.dec[b];
-        if (d.mode == kModeNone || (d.status & SD_ROW_NOISE_OVERRUN)) return;
-        mst = P.rowstat[b * P.slots + d.slot];
-        if (d.mode == kModeResid && !P.draft_is_probs) msd = P.rowstat[b * P.slots + P.n_tslots + d.slot];
-    }
-    if (d.mode == kModeResid) resid_body<TDT, DDT, NZ, EPT, FAST>(P, d, b, c, mst, msd);
-    else prow_body<TDT, NZ, EPT, FAST>(P, d, b, c, mst);
+    const Decision d = P.dec[b];
+    if (d.mode == kModeNone || (d.status & SD_ROW_NOISE_OVERRUN)) return;
+    const float2 mst = P.rowstat[b * P.slots + d.slot];
+    float2 msd = make_float2(0.f, 1.f);
+    if (d.mode == kModeResid && !P.draft_is_probs) msd = P.rowstat[b * P.slots + P.n_tslots + d.slot];
+    if (d.mode == kModeResid) resid_body<TDT, DDT, SD_NOISE_STREAM, EPT, FAST>(P, d, b, c, mst, msd);
+    else prow_body<TDT, SD_NOISE_STREAM, EPT, FAST>(P, d, b, c, mst);
 }
 
-// ------------------------------------------------------------------ k_finalize
-// grid (B), one wave.
-__global__ void __launch_bounds__(64) k_finalize(Plan P) {
-    const int b = blockIdx.x, lane = threadIdx.x;
-    const Decision d = P.dec[b];
-    const int g = P.gamma;
-    int64_t x = -1;
-    float mass = NAN;
-    int32_t status = d.status;
-    if (d.mode != kModeNone && !(status & SD_ROW_NOISE_OVERRUN)) {
-        const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
-        if (d.mode == kModeResid) {
-            // fixed-order residual sum (lane-strided over chunks, then a fixed butterfly)
-            float s = 0.f, wm = 0.f;
-            int overflow = 0;
-            for (int c = lane; c < P.rn_chunks; c += kWave) {
-                s += rp[c].sum;
-                wm = fmaxf(wm, rp[c].wmax);
+// ------------------------------------------------------------------ finalize
+// Σ residual over the chunk partials of sequence b, fixed order (lane-strided, then a butterfly).
+__device__ __forceinline__ float resid_mass(const Plan& P, int b, float* wmax) {
+    const int lane = threadIdx.x & 63;
+    const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
+    float s = 0.f, wm = 0.f;
+    for (int c = lane; c < P.rn_chunks; c += kWave) {
+        s += ld_x(&rp[c].sum, P.coh);
+        if (wmax) wm = fmaxf(wm, ld_x(&rp[c].wmax, P.coh));
+    }
+    if (wmax) *wmax = wave_max(wm);
+    return wave_sum(s);
+}
+
+// The token of sequence b from the argmax-candidate partials (one wave): residual candidates
+// evaluated exactly as fl(fl(res / S) / E), the engine's multinomial(p) fallback, bonus / p-row
+// argmax.  x = -1 when nothing is sampled.
+__device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, float& mass, int32_t& status) {
+    const int lane = threadIdx.x & 63;
+    const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
+    if (d.mode == kModeResid) {
+        int overflow = 0;
+        float wm;
+        const float s = resid_mass(P, b, &wm);
+        mass = s;
+        const int rt = b * P.slots + d.slot;
+        const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+        const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
+        const float2 mst = P.rowstat[rt];
+        if (P.rule == SD_RULE_ENGINE && (double)s <= 1e-12) {
+            // engine/infer_engine.py:319-321: multinomial(p) over the target row (rare: p ~= q)
+            float bv = -INFINITY;
+            int32_t bi = INT_MAX;
+            for (int64_t j = lane; j < P.V; j += kWave) {
+                const float p = prob_dyn(P.tdt, trow, j, P.tT, P.t_keep, kt, mst);
+                const float v = round_dyn(P.tdt, p / round_dyn(P.tdt, exp_noise(P.noise, d.noise_off, b, j)));
+                if (arg_better(v, (int32_t)j, bv, bi)) { bv = v; bi = (int32_t)j; }
             }
-            s = wave_sum(s);
-            wm = wave_max(wm);
-            mass = s;
-            const int rt = b * P.slots + d.slot;
-            const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-            const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
-            const float2 mst = P.rowstat[rt];
-            if (P.rule == SD_RULE_ENGINE && (double)s <= 1e-12) {
-                // engine/infer_engine.py:319-321: multinomial(p) over the target row (rare: p ~= q)
-                float bv = -INFINITY;
-                int32_t bi = INT_MAX;
+            wave_argmax(bv, bi);
+            x = bi;
+            status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
+        } else if (s == 0.f) {
+            // max_fn divides by zero: all-NaN distribution
+            if (P.t_stoch) status |= SD_ROW_INVALID_DIST;
+            else x = 0;   // torch.argmax over an all-NaN row
+        } else {
+            // exact evaluation of the candidates: v = fl(fl(res / S) / E)
+            const float thr = wm * kCandTol;
+            float bv = -INFINITY;
+            int32_t bi = INT_MAX;
+            for (int c = lane; c < P.rn_chunks; c += kWave) {
+                const ResPart& o = rp[c];
+                if (ld_x(&o.wmax, P.coh) < thr) continue;
+                const int nc = ld_x(&o.ncand, P.coh);
+                if (nc > kMaxCand) { overflow = 1; continue; }
+                for (int k = 0; k < nc; ++k) {
+                    const float pr = ld_x(&o.cres[k], P.coh) / s;
+                    const float v = P.t_stoch ? pr / ld_x(&o.ce[k], P.coh) : pr;
+                    const int32_t ci = ld_x(&o.cidx[k], P.coh);
+                    if (arg_better(v, ci, bv, bi)) { bv = v; bi = ci; }
+                }
+            }
+            wave_argmax(bv, bi);
+            // chunks with too many near-equal values (e.g. ties) are re-scanned exactly
+            overflow = __any(overflow);
+            if (overflow) {
+                const void* drow;
+                RowKeep kd{-INFINITY, INT_MAX, 0, 0};
+                float2 msd = make_float2(0.f, 1.f);
+                int ddt = SD_F32;
+                if (P.draft_is_probs) drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
+                else {
+                    const int rd = b * P.slots + P.n_tslots + d.slot;
+                    drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
+                    if (P.d_keep) kd = P.keep[rd];
+                    msd = P.rowstat[rd];
+                    ddt = P.ddt;
+                }
                 for (int64_t j = lane; j < P.V; j += kWave) {
                     const float p = prob_dyn(P.tdt, trow, j, P.tT, P.t_keep, kt, mst);
-                    const float v = round_dyn(P.tdt, p / round_dyn(P.tdt, exp_noise(P.noise, d.noise_off, b, j)));
+                    const float q = P.draft_is_probs ? static_cast<const float*>(drow)[j]
+                                                     : prob_dyn(ddt, drow, j, P.dT, P.d_keep, kd, msd);
+                    const float diff = p - q;
+                    const float rr = diff > 0.f ? diff : 0.f;
+                    const float pr = rr / s;
+                    const float v = P.t_stoch ? pr / exp_noise(P.noise, d.noise_off, b, j) : pr;
                     if (arg_better(v, (int32_t)j, bv, bi)) { bv = v; bi = (int32_t)j; }
                 }
                 wave_argmax(bv, bi);
-                x = bi;
-                status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
-            } else if (s == 0.f) {
-                // max_fn divides by zero: all-NaN distribution
-                if (P.t_stoch) status |= SD_ROW_INVALID_DIST;
-                else x = 0;   // torch.argmax over an all-NaN row
+            }
+            x = bi;
+        }
+    } else {
+        // bonus / p-row: argmax across chunks
+        float pv = -INFINITY;
+        int32_t pi = INT_MAX;
+        for (int c = lane; c < P.rn_chunks; c += kWave) {
+            const float v = ld_x(&rp[c].pval, P.coh);
+            const int32_t i = ld_x(&rp[c].pidx, P.coh);
+            if (arg_better(v, i, pv, pi)) { pv = v; pi = i; }
+        }
+        wave_argmax(pv, pi);
+        x = pi;
+    }
+}
+
+// Outputs of sequence b (one thread): token, mass, engine state (engine/infer_engine.py:307-336
+// applied in place), row status with the threshold flags.
+__device__ void finalize_write(const Plan& P, int b, const Decision& d, int64_t x, float mass, int32_t status,
+                               int64_t acc0) {
+    const int g = P.gamma;
+    P.next_token[b * P.next_token_stride] = x;
+    if (P.resample_mass) P.resample_mass[b] = mass;
+    const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
+    if (engine_state && (status & SD_ROW_DONE)) {
+        int64_t* gen = P.generated + b * P.gen_stride;
+        if (d.mode == kModeResid && x >= 0) {
+            gen[P.step + d.n] = x;
+            if (is_stop(P, x)) status |= SD_ROW_FINISHED;
+        }
+        if (d.n < g)
+            for (int t = P.step + d.n + 1; t < P.step + g; ++t) gen[t] = 0;
+        if (status & SD_ROW_FINISHED) P.finished[b] = 1;
+        P.accepted_count[b] = acc0 + d.n;
+    } else if (P.rule == SD_RULE_ENGINE && d.mode == kModeResid && x >= 0 && is_stop(P, x)) {
+        status |= SD_ROW_FINISHED;
+    }
+    if (P.t_keep)
+        for (int s2 = 0; s2 < P.n_tslots; ++s2) status |= P.keep[b * P.slots + s2].flags;
+    if (P.d_keep)
+        for (int s2 = P.n_tslots; s2 < P.slots; ++s2) status |= P.keep[b * P.slots + s2].flags;
+    P.row_status[b] = status;
+}
+
+// STREAM mode: grid (B), one wave.
+__global__ void __launch_bounds__(64) k_finalize(Plan P) {
+    const int b = blockIdx.x;
+    const Decision d = P.dec[b];
+    int64_t x = -1;
+    float mass = NAN;
+    int32_t status = d.status;
+    if (d.mode != kModeNone && !(status & SD_ROW_NOISE_OVERRUN)) pick_wave(P, b, d, x, mass, status);
+    if (threadIdx.x == 0) {
+        const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
+        finalize_write(P, b, d, x, mass, status, engine_state && (status & SD_ROW_DONE) ? P.accepted_count[b] : 0);
+    }
+}
+
+// ------------------------------------------------------------------ k_sample (PHILOX / perf mode)
+// The row to sample from and its weights: RESID -> (p_n - q_n)+ (max_fn's numerator,
+// sampling/speculative_decoding.py:180-186, engine/infer_engine.py:313-324); BONUS / PROW -> p.
+struct PairRows {
+    const void* trow;
+    const void* drow;
+    RowKeep kt, kd;
+    float2 mst, msd;
+    float t_inv, d_inv;
+    float tT, dT;
+    int32_t V;
+    bool t_al, d_al, resid, t_keep, d_keep, dprobs;
+};
+
+template <int TDT, int DDT>
+__device__ __forceinline__ PairRows pair_rows(const Plan& P, const Decision& d, int b) {
+    PairRows R;
+    R.resid = d.mode == kModeResid;
+    const int rt = b * P.slots + d.slot;
+    R.trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
+    R.kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    R.kd = RowKeep{-INFINITY, INT_MAX, 0, 0};
+    R.mst = P.rowstat[rt];
+    R.msd = make_float2(0.f, 1.f);
+    R.drow = nullptr;
+    if (R.resid) {
+        if (P.draft_is_probs) {
+            R.drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
+        } else {
+            const int rd = b * P.slots + P.n_tslots + d.slot;
+            R.drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
+            if (P.d_keep) R.kd = P.keep[rd];
+            R.msd = P.rowstat[rd];
+        }
+    }
+    R.t_al = (reinterpret_cast<uintptr_t>(R.trow) & 15) == 0;
+    R.d_al = (reinterpret_cast<uintptr_t>(R.drow) & 15) == 0;
+    R.t_inv = 1.0f / R.mst.y;
+    R.d_inv = 1.0f / R.msd.y;
+    R.tT = P.tT;
+    R.dT = P.dT;
+    R.V = P.V;
+    R.t_keep = P.t_keep;
+    R.d_keep = P.d_keep;
+    R.dprobs = P.draft_is_probs;
+    return R;
+}
+
+template <int TDT, int DDT>
+struct PairVec {
+    static constexpr int kVec = Elem<TDT>::kVec < Elem<DDT>::kVec ? Elem<TDT>::kVec : Elem<DDT>::kVec;
+};
+
+// weights of the VEC elements starting at e0 (0 past the vocabulary)
+template <int TDT, int DDT, bool FAST>
+__device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, float* w, float* pw = nullptr) {
+    constexpr int VEC = PairVec<TDT, DDT>::kVec;
+    float xt[VEC], xd[VEC];
+    load_vecn<TDT, VEC>(R.trow, e0, R.V, R.t_al, xt);
+    if (R.resid) {
+        load_vecn<DDT, VEC>(R.drow, e0, R.V, R.d_al, xd);   // dprobs dispatches DDT = F32
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        const int64_t j = e0 + k;
+        const float yt = FAST ? xt[k] : process_value<TDT>(xt[k], j, R.tT, R.t_keep, R.kt);
+        const float p = prob_exact<TDT>(yt, R.mst.x, R.mst.y, R.t_inv);
+        float v = p;
+        if (R.resid) {
+            float q;
+            if (R.dprobs) {
+                q = xd[k];
             } else {
-                // exact evaluation of the candidates: v = fl(fl(res / S) / E)
-                const float thr = wm * kCandTol;
-                float bv = -INFINITY;
-                int32_t bi = INT_MAX;
-                for (int c = lane; c < P.rn_chunks; c += kWave) {
-                    const ResPart& o = rp[c];
-                    if (o.wmax < thr) continue;
-                    if (o.ncand > kMaxCand) { overflow = 1; continue; }
-                    for (int k = 0; k < o.ncand; ++k) {
-                        const float pr = o.cres[k] / s;
-                        const float v = P.t_stoch ? pr / o.ce[k] : pr;
-                        if (arg_better(v, o.cidx[k], bv, bi)) { bv = v; bi = o.cidx[k]; }
-                    }
-                }
-                wave_argmax(bv, bi);
-                // chunks with too many near-equal values (e.g. ties) are re-scanned exactly
-                overflow = __any(overflow);
-                if (overflow) {
-                    const void* drow;
-                    RowKeep kd{-INFINITY, INT_MAX, 0, 0};
-                    float2 msd = make_float2(0.f, 1.f);
-                    int ddt = SD_F32;
-                    if (P.draft_is_probs) drow = static_cast<const float*>(P.drow[d.slot]) + b * P.dstride;
-                    else {
-                        const int rd = b * P.slots + P.n_tslots + d.slot;
-                        drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
-                        if (P.d_keep) kd = P.keep[rd];
-                        msd = P.rowstat[rd];
-                        ddt = P.ddt;
-                    }
-                    for (int64_t j = lane; j < P.V; j += kWave) {
-                        const float p = prob_dyn(P.tdt, trow, j, P.tT, P.t_keep, kt, mst);
-                        const float q = P.draft_is_probs ? static_cast<const float*>(drow)[j]
-                                                         : prob_dyn(ddt, drow, j, P.dT, P.d_keep, kd, msd);
-                        const float diff = p - q;
-                        const float rr = diff > 0.f ? diff : 0.f;
-                        const float pr = rr / s;
-                        const float v = P.t_stoch ? pr / exp_noise(P.noise, d.noise_off, b, j) : pr;
-                        if (arg_better(v, (int32_t)j, bv, bi)) { bv = v; bi = (int32_t)j; }
-                    }
-                    wave_argmax(bv, bi);
-                }
-                x = bi;
+                const float yd = FAST ? xd[k] : process_value<DDT>(xd[k], j, R.dT, R.d_keep, R.kd);
+                q = prob_exact<DDT>(yd, R.msd.x, R.msd.y, R.d_inv);
+            }
+            const float diff = p - q;
+            v = diff > 0.f ? diff : 0.f;
+        }
+        w[k] = j < R.V ? v : 0.f;
+        if (pw) pw[k] = j < R.V ? p : 0.f;
+    }
+}
+
+// Inverse-CDF draw of sequence b (whole workgroup, after all chunk sums landed): a Philox U[0,1)
+// at 53 bits picks the chunk on the fp64 running sum of the chunk totals (lw: staged in LDS),
+// then the element on an fp64 prefix over the chunk's weights (recomputed bit-identically).
+// Every element's interval has its exact fp32 weight as width, so the draw is w_j / Σw up to the
+// rounding of the chunk totals (~1e-7 relative) — no per-element noise.  -1: no positive weight.
+template <int TDT, int DDT, bool FAST, int EPT>
+__device__ __forceinline__ int64_t cdf_pick(const Plan& P, const PairRows& R, int b, const float* lw, int wg_id) {
+    constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC, NW = kThreads / kWave;
+    __shared__ int s_chunk;
+    __shared__ double s_t;
+    __shared__ double s_wtot[NW];
+    __shared__ int s_pos[NW], s_lastp[NW];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (w == 0) {
+        // the chunk: first whose fp64 running total (chunk order) exceeds t = u * total
+        const double u = cdf_uniform(P.noise, (uint32_t)b);
+        int chunk = -1, lastpos = -1;
+        double excl = 0.0, t = 0.0;
+        double total = 0.0;
+        for (int c0 = 0; c0 < P.rn_chunks; c0 += kWave) {   // pass 1 (one group for V <= 128 Ki)
+            const float sv = c0 + lane < P.rn_chunks ? lw[c0 + lane] : 0.f;
+            total = lane_d(total + wave_incl_scan_d((double)sv), 63);
+        }
+        t = u * total;
+        double base = 0.0;
+        for (int c0 = 0; c0 < P.rn_chunks && chunk < 0; c0 += kWave) {
+            const float sv = c0 + lane < P.rn_chunks ? lw[c0 + lane] : 0.f;
+            const double incl = base + wave_incl_scan_d((double)sv);
+            const uint64_t hit = __ballot(incl > t && sv > 0.f);
+            const uint64_t pos = __ballot(sv > 0.f);
+            if (pos) lastpos = c0 + 63 - __builtin_clzll(pos);
+            if (hit) {
+                const int l = __builtin_ctzll(hit);
+                chunk = c0 + l;
+                excl = l > 0 ? lane_d(incl, l - 1) : base;
+            }
+            base = lane_d(incl, 63);
+        }
+        if (lane == 0) {
+            // rounding can leave t at/after the total: take the last positive chunk's end
+            s_chunk = chunk >= 0 ? chunk : lastpos;
+            s_t = chunk >= 0 ? t - excl : INFINITY;
+        }
+    }
+    __syncthreads();
+    SD_TS(wg_id, 7);
+    const int c = s_chunk;
+    if (c < 0) return -1;
+    const double t = s_t;
+    const int64_t base = (int64_t)c * P.rchunk;
+    float wv[EPT];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv + v * VEC);
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) tot += (double)wv[k];
+    SD_TS(wg_id, 8);
+    // exclusive fp64 prefix of the thread totals in thread order: DPP scan, wave offsets via LDS
+    const double wincl = wave_incl_scan_d(tot);
+    double excl = dpp_d<0x138, 0xF, true>(0.0, wincl);   // wave_shr:1 -> the previous lane's inclusive
+    if (lane == 63) s_wtot[w] = wincl;
+    __syncthreads();
+    SD_TS(wg_id, 9);
+    for (int k = 0; k < w; ++k) excl += s_wtot[k];
+    // the thread whose interval [excl, excl + its weights) holds t finds the element
+    int mypos = INT_MAX, lastp = -1;
+    double run = excl;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        run += (double)wv[k];
+        if (wv[k] > 0.f) {
+            lastp = threadIdx.x * EPT + k;
+            if (run > t && mypos == INT_MAX && excl <= t) mypos = threadIdx.x * EPT + k;
+        }
+    }
+    const uint64_t hm = __ballot(mypos != INT_MAX), lm = __ballot(lastp >= 0);
+    if (lane == (hm ? __builtin_ctzll(hm) : 0)) s_pos[w] = hm ? mypos : INT_MAX;
+    if (lane == (lm ? 63 - __builtin_clzll(lm) : 0)) s_lastp[w] = lm ? lastp : -1;
+    __syncthreads();
+    SD_TS(wg_id, 10);
+    int pos = INT_MAX, lp = -1;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        pos = s_pos[k] < pos ? s_pos[k] : pos;
+        lp = s_lastp[k] > lp ? s_lastp[k] : lp;
+    }
+    if (pos == INT_MAX) pos = lp;
+    if (pos < 0) return -1;
+    const int tid = pos / EPT, k = pos - tid * EPT, v = k / VEC;
+    return base + ((int64_t)v * kThreads + tid) * VEC + (k - v * VEC);
+}
+
+// Token of sequence b once every chunk partial has landed (whole workgroup): inverse CDF for
+// stochastic rows, the exact argmax-candidate pick for greedy ones; then the outputs and the
+// engine state.  A short chain of memory round trips: engine-state read issued first, all chunk
+// partials staged into LDS in one cooperative load, then the chosen chunk's rows.
+template <int TDT, int DDT, bool FAST, bool STOCH>
+__device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, int b, PairRows R, int wg_id) {
+    constexpr int EPT = 8;
+    const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
+    int64_t acc0 = 0;
+    if (threadIdx.x == 0 && engine_state && (d.status & SD_ROW_DONE)) acc0 = P.accepted_count[b];   // early
+    int64_t x = -1;
+    float mass = NAN;
+    int32_t status = d.status;
+    if constexpr (STOCH) {
+        __shared__ float l_sum[kTailChunks], l_pv[kTailChunks];
+        __shared__ float s_mass;
+        if (d.mode != kModeNone) {
+            const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
+            for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
+                l_sum[k] = ld_x(&rp[k].sum, P.coh);
+                l_pv[k] = ld_x(&rp[k].pval, P.coh);
+            }
+            __syncthreads();
+            if (threadIdx.x < kWave) {   // Σ residual, fixed order (lane-strided, then a butterfly)
+                float sacc = 0.f;
+                for (int k = threadIdx.x; k < P.rn_chunks; k += kWave) sacc += l_sum[k];
+                sacc = wave_sum(sacc);
+                if (threadIdx.x == 0) s_mass = sacc;
+            }
+            __syncthreads();
+            const float S = s_mass;
+            SD_TS(wg_id, 4);
+            // engine/infer_engine.py:319-321: den <= 1e-12 -> multinomial(p) over the target row
+            const bool fallback = d.mode == kModeResid && P.rule == SD_RULE_ENGINE && (double)S <= 1e-12;
+            if (fallback) {
+                R.resid = false;   // same slot, same row stats: weights p
+                status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
+            }
+#ifdef SD_CDF_TWICE   // diagnostic: the same code run twice (a real loop): warm vs cold instruction cache
+#pragma unroll 1
+            for (int rep = 0; rep < 2; ++rep) {
+                x = cdf_pick<TDT, DDT, FAST, EPT>(P, R, b, fallback ? l_pv : l_sum, wg_id);
+                if (rep == 0) SD_TS(wg_id, 11);
+                __syncthreads();
+            }
+#else
+            x = cdf_pick<TDT, DDT, FAST, EPT>(P, R, b, fallback ? l_pv : l_sum, wg_id);
+#endif
+            SD_TS(wg_id, 5);
+            if (d.mode == kModeResid) mass = S;
+            if (x < 0) status |= SD_ROW_INVALID_DIST;   // no positive weight: torch.multinomial raises
+        }
+    } else {
+        if (d.mode != kModeNone && threadIdx.x < kWave) pick_wave(P, b, d, x, mass, status);
+    }
+    if (threadIdx.x == 0) finalize_write(P, b, d, x, mass, status, acc0);
+    SD_TS(wg_id, 6);
+}
+
+__device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
+    Decision d = P.dec[b];
+    if (d.mode < kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) d.mode = kModeNone;
+    return d;
+}
+
+// grid (chunk, B).  STOCH: chunk Σ weight; greedy (!STOCH): the exact argmax-candidate bodies.
+// TAIL: the last workgroup of each sequence runs sample_finish; otherwise k_sample_finish does.
+template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_sample(Plan P) {
+    constexpr int EPT = 8;
+    constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
+    __shared__ float ldsf[8];
+    const int b = blockIdx.y, c = blockIdx.x;
+    const int wg_id = 8192 + blockIdx.y * gridDim.x + blockIdx.x;
+    SD_TS(wg_id, 0);
+    const Decision d = load_decision(P, b);
+    PairRows R{};
+    if (d.mode != kModeNone) {
+        if constexpr (STOCH) {
+            // RESID also sums p: the engine's den <= 1e-12 fallback samples the target row itself
+            R = pair_rows<TDT, DDT>(P, d, b);
+            SD_TS(wg_id, 1);
+            float sum = 0.f, psum = 0.f;
+            const int64_t base = (int64_t)c * P.rchunk;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                float wv[VEC], pv[VEC];
+                pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv, pv);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) { sum += wv[k]; psum += pv[k]; }
+            }
+            const float2 bs = block_reduce2(make_float2(sum, psum), ldsf);
+            if (threadIdx.x == 0) {
+                ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
+                st_coh(&o.sum, bs.x);
+                st_coh(&o.pval, bs.y);
             }
         } else {
-            // bonus / p-row: argmax across chunks
-            float pv = -INFINITY;
-            int32_t pi = INT_MAX;
-            for (int c = lane; c < P.rn_chunks; c += kWave)
-                if (arg_better(rp[c].pval, rp[c].pidx, pv, pi)) { pv = rp[c].pval; pi = rp[c].pidx; }
-            wave_argmax(pv, pi);
-            x = pi;
+            const float2 mst = P.rowstat[b * P.slots + d.slot];
+            const float2 msd = d.mode == kModeResid && !P.draft_is_probs ? P.rowstat[b * P.slots + P.n_tslots + d.slot]
+                                                                         : make_float2(0.f, 1.f);
+            if (d.mode == kModeResid) resid_body<TDT, DDT, SD_NOISE_PHILOX, EPT, FAST>(P, d, b, c, mst, msd);
+            else prow_body<TDT, SD_NOISE_PHILOX, EPT, FAST>(P, d, b, c, mst);
         }
     }
-    if (lane == 0) {
-        P.next_token[b * P.next_token_stride] = x;
-        if (P.resample_mass) P.resample_mass[b] = mass;
-        // engine/infer_engine.py:307-336 applied in place
-        const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
-        if (engine_state && (status & SD_ROW_DONE)) {
-            int64_t* gen = P.generated + b * P.gen_stride;
-            if (d.mode == kModeResid && x >= 0) {
-                gen[P.step + d.n] = x;
-                if (is_stop(P, x)) status |= SD_ROW_FINISHED;
-            }
-            if (d.n < g)
-                for (int t = P.step + d.n + 1; t < P.step + g; ++t) gen[t] = 0;
-            if (status & SD_ROW_FINISHED) P.finished[b] = 1;
-            P.accepted_count[b] += d.n;
-        } else if (P.rule == SD_RULE_ENGINE && d.mode == kModeResid && x >= 0 && is_stop(P, x)) {
-            status |= SD_ROW_FINISHED;
-        }
-        if (P.t_keep)
-            for (int s2 = 0; s2 < P.n_tslots; ++s2) status |= P.keep[b * P.slots + s2].flags;
-        if (P.d_keep)
-            for (int s2 = P.n_tslots; s2 < P.slots; ++s2) status |= P.keep[b * P.slots + s2].flags;
-        P.row_status[b] = status;
+    SD_TS(wg_id, 2);
+    if constexpr (TAIL) {
+        __shared__ int s_last;
+        if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 1, b), (uint32_t)P.rn_chunks);
+        __syncthreads();
+        SD_TS(wg_id, 3);
+        if (!s_last) return;
+        sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, wg_id);
     }
+}
+
+// grid (B): sample_finish as its own launch (no arrival counters)
+template <int TDT, int DDT, bool FAST, bool STOCH>
+__global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
+    const int b = blockIdx.x;
+    SD_TS(16384 - 1 - b, 0);
+    const Decision d = load_decision(P, b);
+    PairRows R{};
+    if (STOCH && d.mode != kModeNone) R = pair_rows<TDT, DDT>(P, d, b);
+    SD_TS(16384 - 1 - b, 1);
+    sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, 16384 - 1 - b);
 }
 
 // ------------------------------------------------------------------ sd_sample kernels
@@ -969,6 +1387,7 @@ int max_chunks(int vocab) { return (vocab + kThreads * kEptSmall - 1) / (kThread
 
 void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     const int nc = max_chunks(vocab);
+    P.cnt = c.take<uint32_t>(2 * (size_t)kCntMax * kCntStride);   // first, at a fixed offset (see kCntMax)
     P.part = c.take<float2>((size_t)rows_total * nc);
     P.rowstat = c.take<float2>(rows_total);
     P.keep = c.take<RowKeep>(rows_total);
@@ -1010,7 +1429,7 @@ void set_rchunks(sd::Plan& P) {
     P.rn_chunks = (P.V + P.rchunk - 1) / P.rchunk;
 }
 
-int32_t launch_stats(const sd::Plan& P, void* stream);
+int32_t launch_stats(const sd::Plan& P, void* stream, bool tail = false);
 
 #define SD_LAUNCH(kern, grid, block, stream, ...)                                             \
     do {                                                                                      \
@@ -1022,19 +1441,24 @@ int32_t launch_stats(const sd::Plan& P, void* stream);
 // errors left behind by earlier, unrelated runtime calls must not be blamed on our launches
 inline void clear_stale_error() { (void)hipGetLastError(); }
 
-template <int DT>
+template <int DT, bool TAIL>
 int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt, void* stream) {
     const dim3 grid(P.n_chunks, P.B * slot_cnt);
-    if (fast) SD_LAUNCH((k_stats<DT, true>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
-    else SD_LAUNCH((k_stats<DT, false>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
+    if (fast) SD_LAUNCH((k_stats<DT, true, TAIL>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
+    else SD_LAUNCH((k_stats<DT, false, TAIL>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
     return SD_OK;
 }
 
-int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, int slot_cnt, void* stream) {
+int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, int slot_cnt, bool tail, void* stream) {
     if (slot_cnt <= 0) return SD_OK;
-    if (dt == SD_BF16) return launch_stats_dt<SD_BF16>(P, fast, slot_lo, slot_cnt, stream);
-    if (dt == SD_F32) return launch_stats_dt<SD_F32>(P, fast, slot_lo, slot_cnt, stream);
-    return launch_stats_dt<SD_F16>(P, fast, slot_lo, slot_cnt, stream);
+    if (tail) {
+        if (dt == SD_BF16) return launch_stats_dt<SD_BF16, true>(P, fast, slot_lo, slot_cnt, stream);
+        if (dt == SD_F32) return launch_stats_dt<SD_F32, true>(P, fast, slot_lo, slot_cnt, stream);
+        return launch_stats_dt<SD_F16, true>(P, fast, slot_lo, slot_cnt, stream);
+    }
+    if (dt == SD_BF16) return launch_stats_dt<SD_BF16, false>(P, fast, slot_lo, slot_cnt, stream);
+    if (dt == SD_F32) return launch_stats_dt<SD_F32, false>(P, fast, slot_lo, slot_cnt, stream);
+    return launch_stats_dt<SD_F16, false>(P, fast, slot_lo, slot_cnt, stream);
 }
 
 template <int TDT, int DDT>
@@ -1043,11 +1467,37 @@ int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
     // FAST: T == 1 and no top-k / nucleus mask on either side (the engine rule, plain softmax)
     const bool fast = P.tT == 1.0f && P.dT == 1.0f && !P.t_keep && !P.d_keep;
     if (P.noise.mode == SD_NOISE_STREAM) {
-        if (fast) SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_STREAM, false, 8, true>), grid, dim3(kThreads), stream, P);
-        else SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_STREAM, false, 8, false>), grid, dim3(kThreads), stream, P);
+        if (fast) SD_LAUNCH((k_resample<TDT, DDT, 8, true>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_resample<TDT, DDT, 8, false>), grid, dim3(kThreads), stream, P);
     } else {
-        if (fast) SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_PHILOX, true, 8, true>), grid, dim3(kThreads), stream, P);
-        else SD_LAUNCH((k_resample<TDT, DDT, SD_NOISE_PHILOX, true, 8, false>), grid, dim3(kThreads), stream, P);
+        if (P.tails) {
+            if (P.t_stoch) {
+                if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true>), grid, dim3(kThreads), stream, P);
+                else SD_LAUNCH((k_sample<TDT, DDT, false, true, true>), grid, dim3(kThreads), stream, P);
+            } else {
+                if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, false, true>), grid, dim3(kThreads), stream, P);
+                else SD_LAUNCH((k_sample<TDT, DDT, false, false, true>), grid, dim3(kThreads), stream, P);
+            }
+        } else {
+            const dim3 fin(P.B);
+            if (P.t_stoch) {
+                if (fast) {
+                    SD_LAUNCH((k_sample<TDT, DDT, true, true, false>), grid, dim3(kThreads), stream, P);
+                    SD_LAUNCH((k_sample_finish<TDT, DDT, true, true>), fin, dim3(kThreads), stream, P);
+                } else {
+                    SD_LAUNCH((k_sample<TDT, DDT, false, true, false>), grid, dim3(kThreads), stream, P);
+                    SD_LAUNCH((k_sample_finish<TDT, DDT, false, true>), fin, dim3(kThreads), stream, P);
+                }
+            } else {
+                if (fast) {
+                    SD_LAUNCH((k_sample<TDT, DDT, true, false, false>), grid, dim3(kThreads), stream, P);
+                    SD_LAUNCH((k_sample_finish<TDT, DDT, true, false>), fin, dim3(kThreads), stream, P);
+                } else {
+                    SD_LAUNCH((k_sample<TDT, DDT, false, false, false>), grid, dim3(kThreads), stream, P);
+                    SD_LAUNCH((k_sample_finish<TDT, DDT, false, false>), fin, dim3(kThreads), stream, P);
+                }
+            }
+        }
     }
     return SD_OK;
 }
@@ -1081,12 +1531,14 @@ int32_t launch_rowsample(const sd::Plan& P, void* stream) {
 }
 
 // Row statistics for every slot: one launch when target and drafter rows share a dtype.
-int32_t launch_stats(const sd::Plan& P, void* stream) {
+// tail: perf-mode decision in the last workgroup per sequence (both launches count arrivals; the
+// second launch starts after the first has finished, so the last arrival is always in it).
+int32_t launch_stats(const sd::Plan& P, void* stream, bool tail) {
     const bool t_fast = P.tT == 1.0f && !P.t_keep, d_fast = P.dT == 1.0f && !P.d_keep;
     if (P.n_dslots == 0 || (P.tdt == P.ddt && t_fast == d_fast))
-        return launch_stats_group(P, P.tdt, t_fast, 0, P.slots, stream);
-    if (int32_t st = launch_stats_group(P, P.tdt, t_fast, 0, P.n_tslots, stream)) return st;
-    return launch_stats_group(P, P.ddt, d_fast, P.n_tslots, P.n_dslots, stream);
+        return launch_stats_group(P, P.tdt, t_fast, 0, P.slots, tail, stream);
+    if (int32_t st = launch_stats_group(P, P.tdt, t_fast, 0, P.n_tslots, tail, stream)) return st;
+    return launch_stats_group(P, P.ddt, d_fast, P.n_tslots, P.n_dslots, tail, stream);
 }
 
 }  // namespace
@@ -1133,6 +1585,9 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         if (!a->draft_rows[t]) return SD_ERR_INVALID;
     if (a->workspace_bytes < sd_verify_workspace_size(a->batch, a->gamma, a->vocab) || !a->workspace)
         return SD_ERR_WORKSPACE;
+    if (a->noise.mode != SD_NOISE_STREAM &&
+        (a->batch > kCntMax || (a->vocab + kThreads * kEptSmall - 1) / (kThreads * kEptSmall) > kTailChunks))
+        return SD_ERR_UNSUPPORTED;
 
     Plan P{};
     P.B = a->batch; P.gamma = a->gamma; P.V = a->vocab; P.rule = a->rule;
@@ -1168,16 +1623,24 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         if (st != SD_OK) return st;
     }
     set_rchunks(P);
-    if (const char* e = getenv("SD_DIAG")) P.diag = atoi(e);
+    const bool perf = P.noise.mode != SD_NOISE_STREAM;
+#ifdef SD_PHASE_TIMING
+    if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
+#endif
+    // perf mode: decision / token in the last-arriving workgroups (tails) or in small own launches
+    P.tails = 1;
+    if (const char* e = getenv("SD_TAILS")) P.tails = atoi(e);
+    P.coh = perf && P.tails;
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
-    if (int32_t st = launch_stats(P, stream)) return st;
+    if (int32_t st = launch_stats(P, stream, perf && P.tails)) return st;
     if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
-    if (P.noise.mode == SD_NOISE_STREAM) {   // parity mode: the reference's serial noise order
+    if (perf && !P.tails) SD_LAUNCH(k_decide_perf, dim3(P.B), dim3(kThreads), stream, P);
+    if (!perf) {   // parity mode: the reference's serial noise order
         SD_LAUNCH(k_decide, dim3(P.B), dim3(256), stream, P);
         SD_LAUNCH(k_walk, dim3(1), dim3(256), stream, P);
     }
-    if (int32_t st = launch_resample(P, stream)) return st;
-    SD_LAUNCH(k_finalize, dim3(P.B), dim3(64), stream, P);
+    if (int32_t st = launch_resample(P, stream)) return st;   // perf mode: k_sample finalizes in its tail
+    if (!perf) SD_LAUNCH(k_finalize, dim3(P.B), dim3(64), stream, P);
     return SD_OK;
 }
 

@@ -28,7 +28,8 @@ SD_ROW_INVALID_DIST = 0x40
 SD_ROW_NOISE_OVERRUN = 0x80
 SD_ROW_NUCLEUS_INEXACT = 0x100
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libspecdec.so")
+# SPECDEC_LIB selects another in-tree build of the same ABI (e.g. the phase-timing variant)
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("SPECDEC_LIB", "libspecdec.so"))
 
 EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify_workspace_size", "sd_verify",
            "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",

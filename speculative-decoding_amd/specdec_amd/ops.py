@@ -69,7 +69,8 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
     dev = torch.device(device)
     ws = _WS.get(dev)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
+        # zero-filled once: the library keeps its arrival counters (front of the workspace) at zero
+        ws = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
         _WS[dev] = ws
     return ws
 

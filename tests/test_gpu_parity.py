@@ -286,6 +286,42 @@ def test_engine_verify_matches_oracle(sd, B, gamma, V, dtype, seed):
         note_divergence("exact", f"engine seed={seed}")
 
 
+@pytest.mark.parametrize("B,V,dtype,seed", [(6, 4096, torch.bfloat16, 60), (4, 50257, torch.float32, 61),
+                                            (8, 128256, torch.bfloat16, 62)])
+def test_engine_verify_draft_probs(sd, B, V, dtype, seed):
+    """The reference's q buffer handed over as fp32 probabilities (draft_is_probs): mixed-width
+    rows (bf16 target, fp32 drafter) must match the oracle fed the same q."""
+    plain = ref.Processor("multinomial", 1.0)
+    gamma = 4
+    tl, dl, ids = draft_case(B, gamma, V, dtype, seed, plain)
+    tl = tl[:, :gamma]
+    q = ref.softmax(dl, True).float()
+    g1 = torch.Generator().manual_seed(3000 + seed)
+    n_o = {}
+    for exact in (False, True):
+        g1 = torch.Generator().manual_seed(3000 + seed)
+        gen_o = torch.zeros(B, gamma * 2, dtype=torch.long)
+        n_o[exact] = (ref.engine_verify_rows(ref.softmax(tl, exact), q, ids, torch.zeros(B, dtype=torch.bool), [],
+                                             0, gen_o, torch.zeros(B, dtype=torch.long), ref.TorchNoise(g1), exact),
+                      gen_o[:, :gamma], g1.get_state())
+    g2 = torch.Generator().manual_seed(3000 + seed)
+    tld, qd = tl.to(DEV), q.to(DEV)
+    out = sd.ops.verify([tld[:, t, :] for t in range(gamma)], [qd[:, d, :] for d in range(gamma)], ids.to(DEV),
+                        sd.lib.SD_RULE_ENGINE, sd.ops.PLAIN_SOFTMAX, sd.ops.PLAIN_SOFTMAX, sd.StreamNoise(g2),
+                        torch.tensor([], dtype=torch.long, device=DEV), draft_is_probs=True)
+    n_h = out.n_accepted.cpu().tolist()
+    x_h = out.next_token.cpu().tolist()
+
+    def same(r):
+        n, gen, state = r
+        xs = [int(gen[b, n[b]]) if n[b] < gamma else -1 for b in range(B)]
+        return n_h == n and x_h == xs and torch.equal(g2.get_state(), state)
+
+    if not same(n_o[False]):
+        assert same(n_o[True]), (n_h, x_h, n_o[True][0])
+        note_divergence("exact", f"engine probs seed={seed}")
+
+
 # ---------------------------------------------------------------- sample / probs kernels
 @pytest.mark.parametrize("kind", list(KINDS))
 @pytest.mark.parametrize("dtype,V,R", [(torch.bfloat16, 4096, 3), (torch.float32, 50257, 2),
