@@ -74,17 +74,22 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import specdec_amd
-    from specdec_amd import _lib, ops
+    from specdec_amd import _lib, dp, ops
     from specdec_amd.noise import PhiloxNoise
 
-    B, g, V = args.batch, args.gamma, args.vocab
+    # weak scaling: the global batch is args.batch rows per rank, split contiguously by row
+    # (specdec_amd/dp.py); Philox noise is keyed by the global row id, so the shards draw what
+    # one GPU verifying the whole batch would draw for the same rows.  No data-path collective.
+    g, V = args.gamma, args.vocab
+    row0, row1 = dp.shard_rows(args.batch * world, world, rank)
+    B = row1 - row0
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     tl = (torch.randn(B, g, V, generator=gen, device=dev) * 3.0).to(torch.bfloat16)
     dl = (tl.float() + args.sigma * torch.randn(B, g, V, generator=gen, device=dev)).to(torch.bfloat16)
-    noise = PhiloxNoise(seed=4242 + rank)
+    noise = PhiloxNoise(seed=4242)
     draft = torch.empty(B, g, dtype=torch.long, device=dev)
     for d in range(g):   # draft ids drawn from the drafter distribution (untimed setup)
-        tok, _, _ = ops.sample_rows(dl[:, d, :], ops.PLAIN_SOFTMAX, noise)
+        tok, _, _ = ops.sample_rows(dl[:, d, :], ops.PLAIN_SOFTMAX, noise, row_base=row0)
         draft[:, d] = tok
     stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
     trows = [tl[:, t, :] for t in range(g)]
@@ -92,7 +97,7 @@ def main():
 
     def step(prof=None):
         return ops.verify(trows, drows, draft, _lib.SD_RULE_ENGINE, ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise,
-                          stops, prof_events=prof)
+                          stops, prof_events=prof, row_base=row0)
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -127,14 +132,8 @@ def main():
     resid = sum(int(((o.row_status & _lib.SD_ROW_RESIDUAL) != 0).sum()) for o in outs)
     tokens = (acc + resid) * replays
     drafted = B * g * G * replays
-    stats = torch.tensor([elapsed, float(tokens), float(acc * replays), float(drafted)], dtype=torch.float64,
-                         device=dev)
-    if dist:
-        t_max = stats[:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
-        dist.all_reduce(stats, op=dist.ReduceOp.SUM)
-        stats[0] = t_max[0]
-    elapsed, tokens, accepted, drafted = stats.tolist()
+    elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens, "accepted": acc * replays, "drafted": drafted}, dev, dist)
+    tokens, accepted, drafted = tot["tokens"], tot["accepted"], tot["drafted"]
 
     # dominant kernel: row statistics (reads every logit row once); HIP events on its stream
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.prof_steps)]
@@ -177,7 +176,7 @@ def main():
             "dtype": "bf16",
             "data": "synthetic (target logits ~ N(0,3^2), drafter = target + N(0,1), draft ids sampled from the drafter)",
             "config": {"workload": "configs[2]: Llama-3-8B/3.2-1B logit shapes, engine verify step (rule A10)",
-                       "rows_per_gpu": B, "global_batch": B * world, "gamma": g, "vocab": V,
+                       "rows_per_gpu": args.batch, "global_batch": args.batch * world, "gamma": g, "vocab": V,
                        "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G},
             "acceptance_rate": accepted / drafted,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 1
+#define SD_ABI_VERSION 2
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -83,6 +83,9 @@ typedef struct {
     int64_t n_words;         /* STREAM: capacity; overrun => row_status SD_ROW_NOISE_OVERRUN  */
     uint64_t seed;           /* PHILOX: key                                                   */
     uint64_t offset;         /* PHILOX: per-call counter offset (caller advances it)          */
+    int64_t row_base;        /* PHILOX: global id of row 0 of this call — noise is keyed by
+                                (seed, offset, global row), so a batch sharded across ranks
+                                draws exactly what one call over the whole batch draws     */
 } sd_noise;
 
 /* row_status bits */

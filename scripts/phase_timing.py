@@ -48,7 +48,7 @@ for rep in range(3):
     torch.cuda.synchronize()
     t = ts.view(-1, 16).cpu().numpy().astype(np.int64)
     print(f"--- rep {rep}")
-    for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "loop_end", "arrived", "decided"]),
+    for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "loop_end", "arrived", "decided", "dec_stats", "dec_ratios"]),
                                  ("k_sample_finish", 16384 - 64, 16384, ["start", "prologue", "body_end", "arrived",
                                                             "tail_S", "cdf_pick", "finalized", "cdf_select",
                                                             "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"]),

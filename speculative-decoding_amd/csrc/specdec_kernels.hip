@@ -39,6 +39,7 @@ struct Decision {
     int64_t noise_off;  // STREAM: word offset of the Exp noise; PHILOX: unused
     int32_t stop_index;
     int32_t pad;
+    float2 mst, msd;    // PHILOX: (max, Σexp) of the target / drafter row sampled from (k_sample)
 };
 enum { kModeNone = 0, kModeBonus = 1, kModeResid = 2, kModePRow = 3 };
 
@@ -145,6 +146,15 @@ __device__ __forceinline__ bool is_stop(const Plan& P, int64_t tok) {
     return false;
 }
 
+// stop list staged in LDS by a tail (nullptr / too many stops: the global list)
+constexpr int kLdsStops = 64;
+__device__ __forceinline__ bool is_stop_l(const Plan& P, int64_t tok, const int64_t* lstops) {
+    if (!lstops || P.n_stop > kLdsStops) return is_stop(P, tok);
+    for (int k = 0; k < P.n_stop; ++k)
+        if (lstops[k] == tok) return true;
+    return false;
+}
+
 // ------------------------------------------------------------------ block helpers
 struct FMax {
     static constexpr float kId = -INFINITY;
@@ -219,7 +229,7 @@ __device__ __forceinline__ const void* slot_row(const Plan& P, int b, int s) {
     return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
 }
 
-__device__ void decide_seq(const Plan& P, int b, float pf_xt, float pf_xd);
+__device__ void decide_seq(const Plan& P, int b, int64_t pf_tok, float pf_xt, float pf_xd, int wg_id);
 __device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd);
 
 // Arrival at a per-sequence counter (thread 0, after storing its partials with st_coh): true for
@@ -348,7 +358,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
         __syncthreads();
         SD_TS(wg_id, 2);
         if (s_last) {
-            decide_seq(P, b, pf_xt, pf_xd);
+            decide_seq(P, b, pf_tok, pf_xt, pf_xd, wg_id);
             SD_TS(wg_id, 3);
         }
     }
@@ -437,10 +447,10 @@ __device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* x
 
 // p(x_i), q(x_i) from the fetched raw values and the row stats (threads < γ; after a barrier)
 __device__ void seq_ratios_from(const Plan& P, int b, const float2* lstat, const float* lxt, const float* lxd,
-                                float* lp, float* lq) {
+                                float* lp, float* lq, const int64_t* ltok) {
     if (threadIdx.x >= P.gamma) return;
     const int i = threadIdx.x;
-    const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
+    const int64_t tok = ltok[i];
     float p = 0.f, q = 0.f;
     if (tok >= 0 && tok < P.V) {
         const int rt = b * P.slots + i;
@@ -505,11 +515,22 @@ __device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64
         if (woff >= P.noise.n_words) { *overrun = true; return 0.f; }
         return uniform_from_word(P.noise.words[woff]);
     }
-    return uniform_from_word(philox_block(P.noise, (uint32_t)b, kSiteAccept, (uint32_t)i).x);
+    const uint4 q = philox_block(P.noise, (uint32_t)b, kSiteAccept, (uint32_t)(i >> 2));   // 4 drafts per block
+    return uniform_from_word((i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w);
+}
+
+// accept test of draft i given p(x_i), q(x_i) and its uniform
+__device__ __forceinline__ bool accept_draft(const Plan& P, float p, float q, float u) {
+    if (P.rule == SD_RULE_SPEC) return !(u > p / q);   // sampling/speculative_decoding.py:141-145 (fp32)
+    const double ap = (double)q <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)q);   // infer_engine.py:303-305
+    return (double)u < ap;
 }
 
 // The accept rule for one sequence given p(x_i), q(x_i); woff = its first noise word (STREAM).
-__device__ Decision walk_core(const Plan& P, int b, const float* rp, const float* rq, int64_t woff, int64_t* used_out) {
+// lacc (perf mode, nullable): accept flags of the γ drafts precomputed in parallel (decide_seq)
+// lstop (nullable): per-draft "is a stop token" flags, precomputed alongside lacc
+__device__ Decision walk_core(const Plan& P, int b, const float* rp, const float* rq, int64_t woff, int64_t* used_out,
+                              const uint8_t* lacc = nullptr, const uint8_t* lstop = nullptr) {
     Decision d{};
     d.stop_index = -1;
     d.noise_off = 0;
@@ -521,15 +542,14 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
         // sampling/speculative_decoding.py:139-145: r = rand(γ'); n = first i with r_i > p_i/q_i
         int n = g;
         for (int i = 0; i < g; ++i) {
-            const float r = draw_uniform(P, b, i, woff + i, &overrun);
-            const float frac = rp[i] / rq[i];
-            if (r > frac && n == g) n = i;
+            const bool acc = lacc ? lacc[i] != 0 : accept_draft(P, rp[i], rq[i], draw_uniform(P, b, i, woff + i, &overrun));
+            if (!acc && n == g) n = i;
         }
         used = g;
         d.n = n;
         // :150-155 stop token among the accepted drafts -> the reference returns before sampling
         for (int j = 0; j < n; ++j)
-            if (is_stop(P, P.draft_tokens[b * P.tok_stride + j])) { d.stop_index = j; break; }
+            if (lstop ? lstop[j] != 0 : is_stop(P, P.draft_tokens[b * P.tok_stride + j])) { d.stop_index = j; break; }
         if (d.stop_index >= 0) {
             d.mode = kModeNone;
             d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
@@ -548,14 +568,14 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
         if (act) {
             d.status = SD_ROW_DONE;
             for (int i = 0; i < g; ++i) {
-                const int64_t tok = P.draft_tokens[b * P.tok_stride + i];
-                const double p = rp[i], q = rq[i];
-                const double ap = q <= 0.0 ? 1.0 : fmin(1.0, p / q);
-                const float u = draw_uniform(P, b, i, woff + used, &overrun);
+                const bool acc = lacc ? lacc[i] != 0 : accept_draft(P, rp[i], rq[i], draw_uniform(P, b, i, woff + used, &overrun));
                 used += 1;
-                if ((double)u < ap) {
+                if (acc) {
                     d.n += 1;
-                    if (is_stop(P, tok)) { d.status |= SD_ROW_FINISHED; break; }
+                    if (lstop ? lstop[i] != 0 : is_stop(P, P.draft_tokens[b * P.tok_stride + i])) {
+                        d.status |= SD_ROW_FINISHED;
+                        break;
+                    }
                 } else {
                     d.mode = kModeResid;
                     d.slot = i;
@@ -608,17 +628,35 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
 // Perf-mode decision of sequence b by one 256-thread workgroup (the k_stats tail): row stats
 // from the partials (published to rowstat for the sampling pass), p/q at the drafted ids, the
 // accept walk on Philox uniforms.
-__device__ void decide_seq(const Plan& P, int b, float pf_xt, float pf_xd) {
+__device__ void decide_seq(const Plan& P, int b, int64_t pf_tok, float pf_xt, float pf_xd, int wg_id) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
     __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA], lxt[SD_MAX_GAMMA], lxd[SD_MAX_GAMMA];
-    if (threadIdx.x < P.gamma) { lxt[threadIdx.x] = pf_xt; lxd[threadIdx.x] = pf_xd; }   // prefetched
+    __shared__ int64_t ltok[SD_MAX_GAMMA];
+    __shared__ uint8_t lstop[SD_MAX_GAMMA];
+    if (threadIdx.x < P.gamma) {   // prefetched by the caller; stop flags now, overlapping seq_stats
+        ltok[threadIdx.x] = pf_tok;
+        lxt[threadIdx.x] = pf_xt;
+        lxd[threadIdx.x] = pf_xd;
+        lstop[threadIdx.x] = is_stop(P, pf_tok);
+    }
     seq_stats(P, b, lstat, true);       // every wave reduces partials
     __syncthreads();
-    seq_ratios_from(P, b, lstat, lxt, lxd, lp, lq);
+    SD_TS(wg_id, 4);
+    seq_ratios_from(P, b, lstat, lxt, lxd, lp, lq, ltok);
+    __shared__ uint8_t lacc[SD_MAX_GAMMA];
+    if (threadIdx.x < P.gamma) {   // every draft's uniform and accept test in parallel
+        bool ovr = false;
+        lacc[threadIdx.x] = accept_draft(P, lp[threadIdx.x], lq[threadIdx.x], draw_uniform(P, b, threadIdx.x, 0, &ovr));
+    }
     __syncthreads();
+    SD_TS(wg_id, 5);
     if (threadIdx.x == 0) {
         int64_t used;
-        const Decision d = walk_core(P, b, lp, lq, 0, &used);
+        Decision d = walk_core(P, b, lp, lq, 0, &used, lacc, lstop);
+        if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision
+            d.mst = lstat[d.slot];
+            d.msd = d.mode == kModeResid && !P.draft_is_probs ? lstat[P.n_tslots + d.slot] : make_float2(0.f, 1.f);
+        }
         publish_decision(P, b, d);
         if (P.words_used && b == 0) *P.words_used = 0;
     }
@@ -628,8 +666,12 @@ __device__ void decide_seq(const Plan& P, int b, float pf_xt, float pf_xd) {
 __global__ void __launch_bounds__(kThreads) k_decide_perf(Plan P) {
     const int b = blockIdx.x;
     float xt = 0.f, xd = 0.f;
-    if (threadIdx.x < P.gamma) fetch_drafted(P, b, threadIdx.x, P.draft_tokens[b * P.tok_stride + threadIdx.x], &xt, &xd);
-    decide_seq(P, b, xt, xd);
+    int64_t tok = -1;
+    if (threadIdx.x < P.gamma) {
+        tok = P.draft_tokens[b * P.tok_stride + threadIdx.x];
+        fetch_drafted(P, b, threadIdx.x, tok, &xt, &xd);
+    }
+    decide_seq(P, b, tok, xt, xd, 8192 - 1 - b);
 }
 
 // ------------------------------------------------------------------ k_resample
@@ -894,7 +936,7 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
 // Outputs of sequence b (one thread): token, mass, engine state (engine/infer_engine.py:307-336
 // applied in place), row status with the threshold flags.
 __device__ void finalize_write(const Plan& P, int b, const Decision& d, int64_t x, float mass, int32_t status,
-                               int64_t acc0) {
+                               int64_t acc0, const int64_t* lstops = nullptr) {
     const int g = P.gamma;
     P.next_token[b * P.next_token_stride] = x;
     if (P.resample_mass) P.resample_mass[b] = mass;
@@ -903,13 +945,13 @@ __device__ void finalize_write(const Plan& P, int b, const Decision& d, int64_t 
         int64_t* gen = P.generated + b * P.gen_stride;
         if (d.mode == kModeResid && x >= 0) {
             gen[P.step + d.n] = x;
-            if (is_stop(P, x)) status |= SD_ROW_FINISHED;
+            if (is_stop_l(P, x, lstops)) status |= SD_ROW_FINISHED;
         }
         if (d.n < g)
             for (int t = P.step + d.n + 1; t < P.step + g; ++t) gen[t] = 0;
         if (status & SD_ROW_FINISHED) P.finished[b] = 1;
         P.accepted_count[b] = acc0 + d.n;
-    } else if (P.rule == SD_RULE_ENGINE && d.mode == kModeResid && x >= 0 && is_stop(P, x)) {
+    } else if (P.rule == SD_RULE_ENGINE && d.mode == kModeResid && x >= 0 && is_stop_l(P, x, lstops)) {
         status |= SD_ROW_FINISHED;
     }
     if (P.t_keep)
@@ -955,7 +997,7 @@ __device__ __forceinline__ PairRows pair_rows(const Plan& P, const Decision& d, 
     R.trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
     R.kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
     R.kd = RowKeep{-INFINITY, INT_MAX, 0, 0};
-    R.mst = P.rowstat[rt];
+    R.mst = d.mst;   // perf mode: carried by the decision (no dependent rowstat load)
     R.msd = make_float2(0.f, 1.f);
     R.drow = nullptr;
     if (R.resid) {
@@ -965,7 +1007,7 @@ __device__ __forceinline__ PairRows pair_rows(const Plan& P, const Decision& d, 
             const int rd = b * P.slots + P.n_tslots + d.slot;
             R.drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
             if (P.d_keep) R.kd = P.keep[rd];
-            R.msd = P.rowstat[rd];
+            R.msd = d.msd;
         }
     }
     R.t_al = (reinterpret_cast<uintptr_t>(R.trow) & 15) == 0;
@@ -1119,6 +1161,8 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
     const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
     int64_t acc0 = 0;
     if (threadIdx.x == 0 && engine_state && (d.status & SD_ROW_DONE)) acc0 = P.accepted_count[b];   // early
+    __shared__ int64_t lstops[kLdsStops];   // wave 0 stages the stop list (read by thread 0 at the end)
+    if (threadIdx.x < P.n_stop && threadIdx.x < kLdsStops) lstops[threadIdx.x] = P.stops[threadIdx.x];
     int64_t x = -1;
     float mass = NAN;
     int32_t status = d.status;
@@ -1164,7 +1208,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
     } else {
         if (d.mode != kModeNone && threadIdx.x < kWave) pick_wave(P, b, d, x, mass, status);
     }
-    if (threadIdx.x == 0) finalize_write(P, b, d, x, mass, status, acc0);
+    if (threadIdx.x == 0) finalize_write(P, b, d, x, mass, status, acc0, lstops);
     SD_TS(wg_id, 6);
 }
 

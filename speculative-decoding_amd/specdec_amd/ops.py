@@ -86,19 +86,22 @@ def _require_rows(t: torch.Tensor, name: str, V: int) -> None:
         raise ValueError(f"{name}: unsupported dtype {t.dtype}")
 
 
-def _noise_struct(noise, n_words_needed: int, device):
-    """(sd_noise, keepalive tensor) for a call that may consume up to n_words_needed words."""
+def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
+    """(sd_noise, keepalive tensor) for a call that may consume up to n_words_needed words.
+    row_base: global id of the call's row 0 (Philox noise is keyed by the global row)."""
     if isinstance(noise, StreamNoise):
         words = noise.draw(n_words_needed, device)
-        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0), words
+        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0, 0), words
     if isinstance(noise, PhiloxNoise):
-        return _lib.sd_noise(_lib.SD_NOISE_PHILOX, None, 0, noise.seed, noise.next_offset()), None
+        if not 0 <= row_base < (1 << 24):
+            raise ValueError("row_base must be in [0, 2^24)")
+        return _lib.sd_noise(_lib.SD_NOISE_PHILOX, None, 0, noise.seed, noise.next_offset(), row_base), None
     raise TypeError(f"unsupported noise source {type(noise).__name__}")
 
 
 # --------------------------------------------------------------------------- sampling
 def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Tensor] = None,
-                want_prob: bool = False):
+                want_prob: bool = False, row_base: int = 0):
     """LogitsProcessor.__call__ + .sample on every row of logits [R, V] (one sample per row).
 
     Returns (tokens int64 [R], token_prob fp32 [R] or None, row_status int32 [R]).  Under
@@ -114,7 +117,7 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     prob = torch.empty(R, dtype=torch.float32, device=dev) if want_prob else None
     status = torch.empty(R, dtype=torch.int32, device=dev)
     need = 2 * R * V if spec.stochastic else 0
-    nz, keep = _noise_struct(noise, need, dev)
+    nz, keep = _noise_struct(noise, need, dev, row_base)
     nbytes = lib.sd_sample_workspace_size(R, V)
     ws = _workspace(nbytes, dev)
     a = _lib.sd_sample_args(R, V, logits.data_ptr(), logits.stride(0), _DT[logits.dtype], spec.struct(), nz,
@@ -162,13 +165,15 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
            rule: int, target_proc, draft_proc, noise, stop_tokens: Optional[torch.Tensor] = None,
            skip_sample_adjustment: bool = False, draft_is_probs: bool = False,
            active: Optional[torch.Tensor] = None, engine_state: Optional[dict] = None,
-           sync_noise: bool = True, prof_events=None) -> VerifyOut:
+           sync_noise: bool = True, prof_events=None, row_base: int = 0) -> VerifyOut:
     """One verify step for B sequences.
 
     target_rows: γ+1 (SPEC) or γ (ENGINE) tensors [B, V] — row t of every sequence;
     draft_rows:  γ tensors [B, V] (logits, or fp32 probabilities with draft_is_probs);
     draft_tokens: int64 [B, >=γ].  Under StreamNoise the torch generator is advanced by the
     words the kernels consumed, which needs one device->host read (sync_noise).
+    row_base: global row id of this call's row 0 under PhiloxNoise (data-parallel shards draw
+    what one call over the whole batch would draw for the same rows).
     """
     gamma = len(draft_rows)
     if not 1 <= gamma <= _lib.SD_MAX_GAMMA:
@@ -211,7 +216,7 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
                     torch.empty(1, dtype=torch.long, device=dev))
     stochastic = rule == _lib.SD_RULE_ENGINE or tspec.stochastic
     need = B * (gamma + (2 * V if stochastic else 0))
-    nz, keep = _noise_struct(noise, need, dev)
+    nz, keep = _noise_struct(noise, need, dev, row_base)
     ws = _workspace(lib.sd_verify_workspace_size(B, gamma, V), dev)
 
     a = _lib.sd_verify_args()

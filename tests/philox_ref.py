@@ -35,8 +35,9 @@ def block(seed: int, offset: int, row, site: int, idx):
 
 
 def accept_uniform(seed: int, offset: int, row: int, i: int) -> float:
-    """The accept-test uniform of draft i of row `row` (torch.rand's fp32 from one word)."""
-    w = int(block(seed, offset, row, SITE_ACCEPT, i)[0])
+    """The accept-test uniform of draft i of row `row`: word i % 4 of block i // 4 (torch.rand's fp32
+    from one word)."""
+    w = int(block(seed, offset, row, SITE_ACCEPT, i >> 2)[i & 3])
     return np.float32((w & 0xFFFFFF) * 2.0 ** -24)
 
 

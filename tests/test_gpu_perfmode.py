@@ -373,3 +373,26 @@ def test_perf_repeat_and_graph_replay_are_deterministic(sd):
         torch.cuda.synchronize()
         for f, a, b in zip(fields, want, outs):
             assert torch.equal(a, b), f
+
+
+def test_perf_sharded_calls_equal_one_call(sd):
+    """Data-parallel shards: verifying rows [0, 13) and [13, 32) in two calls with
+    row_base = shard start gives exactly the one-call outputs — noise is keyed by the global row."""
+    B, g, V = 32, 4, 8192
+    tl = rand_logits((B, g, V), torch.bfloat16, 61).to(DEV)
+    dl = (tl.float() + rand_logits((B, g, V), torch.float32, 62, 1.0).to(DEV)).to(torch.bfloat16)
+    ids = dl.float().argmax(-1)
+    proc = ref.Processor("multinomial", 1.0)
+    fields = ("n_accepted", "next_token", "row_status")
+    whole = verify(sd, tl, dl, ids, sd.lib.SD_RULE_ENGINE, proc, sd.PhiloxNoise(seed=9, offset=4))
+    parts = []
+    for lo, hi in ((0, 13), (13, 32)):
+        parts.append(verify(sd, tl[lo:hi], dl[lo:hi], ids[lo:hi], sd.lib.SD_RULE_ENGINE, proc,
+                            sd.PhiloxNoise(seed=9, offset=4), row_base=lo))
+    for f in fields:
+        assert torch.equal(getattr(whole, f), torch.cat([getattr(p, f) for p in parts])), f
+    # drafter sampling shards the same way
+    tok_all, _, _ = sd.ops.sample_rows(dl[:, 0], spec_of(sd, proc), sd.PhiloxNoise(seed=3))
+    tok_a, _, _ = sd.ops.sample_rows(dl[:13, 0], spec_of(sd, proc), sd.PhiloxNoise(seed=3))
+    tok_b, _, _ = sd.ops.sample_rows(dl[13:, 0], spec_of(sd, proc), sd.PhiloxNoise(seed=3), row_base=13)
+    assert torch.equal(tok_all, torch.cat([tok_a, tok_b]))

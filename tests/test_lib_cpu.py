@@ -43,7 +43,7 @@ int main(void) {
   F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
   F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end)
   F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes)
-  F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes)
+  F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes) F(sd_noise, row_base)
   return 0;
 }
 """
