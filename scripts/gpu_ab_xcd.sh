@@ -1,0 +1,10 @@
+#!/bin/bash
+# GPU-box recipe: tests, then bench + phase timing with / without XCD-affine placement
+set -eo pipefail
+cd $GRAFT_REPO_ROOT
+timeout -k 10 300 python -m pytest tests/test_gpu_perfmode.py -q -m gpu -x > gpurun_out/gpu_perf_tests.log 2>&1
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1
+for a in 1 0; do
+  SD_XCD_AFFINE=$a timeout -k 10 200 python bench.py --no-cpu-baseline --steps 400 --prof-steps 5 > gpurun_out/bench_x$a.json 2>/dev/null
+  SD_XCD_AFFINE=$a timeout -k 10 200 python scripts/phase_timing.py > gpurun_out/phase_x$a.log 2>&1
+done

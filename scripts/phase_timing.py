@@ -67,6 +67,8 @@ for rep in range(3):
             if len(v):
                 d = (v - t0) / 100.0
                 print(f"  {ph:10s} n={len(v):5d}  min {d.min():7.2f}  p50 {np.median(d):7.2f}  max {d.max():7.2f} us")
+    if rep == 2:   # per-workgroup dump of the k_stats launch for offline analysis
+        np.save(os.path.join(ROOT, "gpurun_out", "phase_kstats.npy"), t[:8192])
     blk = t[8192:16384]
     sel = (blk[:, 4] > 0) & (blk[:, 10] > 0)
     if sel.any():

@@ -99,6 +99,7 @@ struct Plan {
     uint64_t* ts;         // SD_PHASE_TIMING builds only: per-workgroup phase timestamps
     int32_t tails;        // perf mode: decide / finish in last-arrival tails (1) or own launches (0)
     int32_t coh;          // partials may come from the same launch: read them agent-coherently
+    int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
 };
 
 // Phase timestamps (diagnostic builds, -DSD_PHASE_TIMING): thread 0 of workgroup `wg` records
@@ -243,6 +244,18 @@ __device__ __forceinline__ bool arrive_last(uint32_t* ctr, uint32_t total) {
     return true;
 }
 
+// XCD-affine workgroup placement.  Workgroups are dealt round-robin over the 8 XCDs by linear
+// block id, so id % 8 labels an XCD group (MI355X_MICROARCH.md, dispatch).  When B % 8 == 0 the
+// (sequence, item) of block id is chosen with sequence % 8 == id % 8: every workgroup of a
+// sequence — its row-statistics spans, its decision tail, its sampling chunks and their tail —
+// runs on one XCD, so the sampler re-reads the rows (and the tails their partials) from that
+// XCD's L2.  Placement only affects speed: the exchange protocol never assumes it.
+__device__ __forceinline__ void affine_split(int id, int per_seq, int& b, int& item) {
+    const int w = id & 7, k = id >> 3;
+    b = (k / per_seq) * 8 + w;
+    item = k % per_seq;
+}
+
 // <= 80 SGPRs keeps 8 workgroups of 256 threads resident per CU (MI355X_MICROARCH.md, residency)
 // TAIL (perf mode): the last workgroup to finish a sequence's rows runs its decision (decide_seq).
 template <int DT, bool FAST, bool TAIL>
@@ -252,7 +265,17 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
     const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
     SD_TS(wg_id, 0);
-    const int b = blockIdx.y / slot_cnt, s = slot_lo + blockIdx.y % slot_cnt;
+    int b, s, chunk;
+    if (P.xcd_affine) {
+        int item;
+        affine_split(wg_id, slot_cnt * (int)gridDim.x, b, item);
+        s = slot_lo + item / (int)gridDim.x;
+        chunk = item % (int)gridDim.x;
+    } else {
+        b = blockIdx.y / slot_cnt;
+        s = slot_lo + blockIdx.y % slot_cnt;
+        chunk = blockIdx.x;
+    }
     const int r = b * P.slots + s;
     const void* row = slot_row(P, b, s);
     // TAIL: drafted ids now (consumed after the loop), their logits right after it, so a
@@ -263,7 +286,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
     const RowKeep kp = has_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    const int64_t lo = (int64_t)blockIdx.x * P.chunk;
+    const int64_t lo = (int64_t)chunk * P.chunk;
     const int64_t hi = lo + P.chunk < P.V ? lo + P.chunk : P.V;
     const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
     const int nit = (int)((hi - lo + STEP - 1) / STEP);
@@ -350,7 +373,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     if (threadIdx.x == 0) {
         float M = lm[0], S = ls[0];
         for (int k = 1; k < kThreads / kWave; ++k) online_merge(M, S, lm[k], ls[k]);
-        st_coh(P.part + (int64_t)r * P.n_chunks + blockIdx.x, make_float2(M, S));
+        st_coh(P.part + (int64_t)r * P.n_chunks + chunk, make_float2(M, S));
     }
     if constexpr (TAIL) {
         __shared__ int s_last;
@@ -369,12 +392,12 @@ __device__ __forceinline__ float2 combine_row(const Plan& P, int r) {
     const int lane = threadIdx.x & 63;
     const float2* pr = P.part + (int64_t)r * P.n_chunks;
     float m = -INFINITY;
-    for (int c = lane; c < P.n_chunks; c += kWave) m = fmaxf(m, ld_x(pr + c, P.coh).x);
+    for (int c = lane; c < P.n_chunks; c += kWave) m = fmaxf(m, ld_coh(pr + c).x);
     m = wave_max(m);
     // fixed-order sum: lane-strided partial sums, then a fixed butterfly
     float s = 0.f;
     for (int c = lane; c < P.n_chunks; c += kWave) {
-        const float2 v = ld_x(pr + c, P.coh);
+        const float2 v = ld_coh(pr + c);
         if (v.x > -INFINITY) s += v.y * sd_exp(v.x - m);
     }
     s = wave_sum(s);
@@ -408,7 +431,7 @@ __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
 #pragma unroll
         for (int k = 0; k < kMaxSlotsPerWave; ++k) {
             const int s = w + k * nw;
-            v[k] = (s < P.slots && lane < P.n_chunks) ? ld_x(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane, P.coh)
+            v[k] = (s < P.slots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
                                                       : make_float2(-INFINITY, 0.f);
         }
 #pragma unroll
@@ -834,8 +857,8 @@ __device__ __forceinline__ float resid_mass(const Plan& P, int b, float* wmax) {
     const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
     float s = 0.f, wm = 0.f;
     for (int c = lane; c < P.rn_chunks; c += kWave) {
-        s += ld_x(&rp[c].sum, P.coh);
-        if (wmax) wm = fmaxf(wm, ld_x(&rp[c].wmax, P.coh));
+        s += ld_coh(&rp[c].sum);
+        if (wmax) wm = fmaxf(wm, ld_coh(&rp[c].wmax));
     }
     if (wmax) *wmax = wave_max(wm);
     return wave_sum(s);
@@ -879,13 +902,13 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
             int32_t bi = INT_MAX;
             for (int c = lane; c < P.rn_chunks; c += kWave) {
                 const ResPart& o = rp[c];
-                if (ld_x(&o.wmax, P.coh) < thr) continue;
-                const int nc = ld_x(&o.ncand, P.coh);
+                if (ld_coh(&o.wmax) < thr) continue;
+                const int nc = ld_coh(&o.ncand);
                 if (nc > kMaxCand) { overflow = 1; continue; }
                 for (int k = 0; k < nc; ++k) {
-                    const float pr = ld_x(&o.cres[k], P.coh) / s;
-                    const float v = P.t_stoch ? pr / ld_x(&o.ce[k], P.coh) : pr;
-                    const int32_t ci = ld_x(&o.cidx[k], P.coh);
+                    const float pr = ld_coh(&o.cres[k]) / s;
+                    const float v = P.t_stoch ? pr / ld_coh(&o.ce[k]) : pr;
+                    const int32_t ci = ld_coh(&o.cidx[k]);
                     if (arg_better(v, ci, bv, bi)) { bv = v; bi = ci; }
                 }
             }
@@ -924,8 +947,8 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
         float pv = -INFINITY;
         int32_t pi = INT_MAX;
         for (int c = lane; c < P.rn_chunks; c += kWave) {
-            const float v = ld_x(&rp[c].pval, P.coh);
-            const int32_t i = ld_x(&rp[c].pidx, P.coh);
+            const float v = ld_coh(&rp[c].pval);
+            const int32_t i = ld_coh(&rp[c].pidx);
             if (arg_better(v, i, pv, pi)) { pv = v; pi = i; }
         }
         wave_argmax(pv, pi);
@@ -1172,8 +1195,8 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
         if (d.mode != kModeNone) {
             const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
             for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
-                l_sum[k] = ld_x(&rp[k].sum, P.coh);
-                l_pv[k] = ld_x(&rp[k].pval, P.coh);
+                l_sum[k] = ld_coh(&rp[k].sum);
+                l_pv[k] = ld_coh(&rp[k].pval);
             }
             __syncthreads();
             if (threadIdx.x < kWave) {   // Σ residual, fixed order (lane-strided, then a butterfly)
@@ -1225,8 +1248,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     __shared__ float ldsf[8];
-    const int b = blockIdx.y, c = blockIdx.x;
     const int wg_id = 8192 + blockIdx.y * gridDim.x + blockIdx.x;
+    int b, c;
+    if (P.xcd_affine) affine_split(wg_id - 8192, (int)gridDim.x, b, c);
+    else { b = blockIdx.y; c = blockIdx.x; }
     SD_TS(wg_id, 0);
     const Decision d = load_decision(P, b);
     PairRows R{};
@@ -1675,6 +1700,8 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.tails = 1;
     if (const char* e = getenv("SD_TAILS")) P.tails = atoi(e);
     P.coh = perf && P.tails;
+    P.xcd_affine = perf && P.B % 8 == 0;
+    if (const char* e = getenv("SD_XCD_AFFINE")) P.xcd_affine = P.xcd_affine && atoi(e);
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
     if (int32_t st = launch_stats(P, stream, perf && P.tails)) return st;
     if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
