@@ -220,6 +220,41 @@ int32_t sd_sample(const sd_sample_args* args, void* stream);
 size_t sd_probs_workspace_size(int32_t rows, int32_t vocab);
 int32_t sd_probs(const sd_probs_args* args, void* stream);
 
+/* The n-gram-assisted verify step (rule A11, ngram_assisted/ngram_assisted.py:111-164): sample-
+ * and-compare of γ' drafts against the processed target rows, then an independent draw x from the
+ * mismatch row (or the bonus row), no residual.  STREAM noise follows the reference's draw order
+ * (one full-row Exp draw per compare sample, then x: words_used = draws × 2V); filler ids =
+ * topk(filler_k) of every processed row (lowest index first among equal probabilities).        */
+typedef struct {
+    int32_t batch;               /* B (the reference is batch 1)                               */
+    int32_t gamma;               /* γ' drafts, 0..SD_MAX_GAMMA                                  */
+    int32_t vocab;
+    const void* target_rows[SD_MAX_GAMMA + 1];   /* rows 0..γ'-1 verify draft i, row γ' = bonus */
+    int64_t target_stride_b;
+    int32_t target_dtype;
+    const int64_t* draft_tokens; /* [B, >=γ']                                                  */
+    int64_t draft_tokens_stride_b;
+    sd_processor proc;           /* the loop's logits_processor                                */
+    const int64_t* stop_tokens;
+    int32_t n_stop;
+    int32_t filler_k;            /* 0..8                                                       */
+    sd_noise noise;
+    /* outputs, device */
+    int32_t* n_accepted;         /* [B] n                                                      */
+    int64_t* next_token;         /* [B] x, -1 when a stop token among the accepted drafts ends  */
+    int32_t* prune_target;       /* [B] γ'-n+1 on a mismatch (:139-141), else 0                 */
+    int32_t* stop_index;         /* [B] first accepted stop draft, -1                           */
+    int32_t* row_status;         /* [B] SD_ROW_* (BONUS: x from the bonus row; FALLBACK_P: p_n) */
+    int64_t* words_used;         /* [1] STREAM words consumed (batch 1 semantics)               */
+    int64_t* filler_ids;         /* [B, γ'+1, filler_k] at + b * filler_stride_b + i * filler_k */
+    int64_t filler_stride_b;
+    void* workspace;
+    size_t workspace_bytes;
+} sd_ngram_args;
+
+size_t sd_ngram_workspace_size(int32_t batch, int32_t gamma, int32_t vocab);
+int32_t sd_ngram_verify(const sd_ngram_args* args, void* stream);
+
 /* Host side: torch CPU generator state (torch.Generator.get_state(), 5056 bytes) <-> words. */
 int32_t sd_mt19937_fill(const uint8_t* torch_state, size_t state_len, uint32_t* out, int64_t n);
 int32_t sd_mt19937_advance(uint8_t* torch_state, size_t state_len, int64_t n);

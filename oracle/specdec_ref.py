@@ -399,6 +399,133 @@ def ngram_verify_step(target_rows: torch.Tensor, draft_ids: Sequence[int], proc:
     return n, x
 
 
+class NgramStore:
+    """The reference's n-gram drafters (ngram_assisted/ngram_storage.py), restated on explicit
+    generator draws.  kind "one" = OneLevelNGramStorage (:71-150): only (n-1)-grams; kind "multi" =
+    NGramStorage (:154-249): every j-gram for j = min(n-1, len) .. 2, longest known first.
+    counts[j][gram][token] = occurrences, best[j][gram] = the argmax token, which changes only when
+    a count becomes strictly larger than the current best's (first seen wins ties)."""
+
+    def __init__(self, kind: str, n: int, vocab: int, noise: TorchNoise):
+        assert kind in ("one", "multi") and n > 1
+        self.kind, self.n, self.V, self.noise = kind, n, vocab, noise
+        self.counts: dict = {}
+        self.best: dict = {}
+
+    def _orders(self, length: int):
+        if self.kind == "one":
+            return [self.n - 1] if length >= self.n - 1 else []
+        return list(range(min(self.n - 1, length), 1, -1))
+
+    def _add(self, j: int, gram: tuple, tokens: Sequence[int]):
+        cj = self.counts.setdefault(j, {}).setdefault(gram, {})
+        bj = self.best.setdefault(j, {})
+        if gram not in bj:
+            bj[gram] = tokens[0]
+        for tok in tokens:
+            c = cj.get(tok, 0) + 1
+            cj[tok] = c
+            if c > 1 and c > cj[bj[gram]]:
+                bj[gram] = tok
+
+    def next_token(self, seq: List[int]) -> Tuple[int, bool]:
+        # :159 / :80: torch.randint(V, (B,)) is drawn first, whatever the lookup finds
+        out = int(torch.randint(self.V, size=(1,), generator=self.noise.g)[0])
+        if self.kind == "one" and len(seq) < self.n - 1:
+            return out, False
+        for j in self._orders(len(seq)):
+            gram = tuple(seq[-j:])
+            if gram in self.best.get(j, {}):
+                return self.best[j][gram], True
+        return out, False
+
+    def update(self, seq: List[int], tokens: Sequence[int]):
+        # :104-124 / :190-221: "one" needs len >= n; "multi" needs len >= 1
+        if self.kind == "one" and len(seq) < self.n:
+            return
+        if len(seq) < 1:
+            return
+        for j in self._orders(len(seq)):
+            self._add(j, tuple(seq[-j:]), tokens)
+
+    def initialize(self, seq: List[int]):
+        # :126-143 / :223-243: every position of the prompt
+        if self.kind == "one":
+            for i in range(len(seq) - self.n + 1):
+                self._add(self.n - 1, tuple(seq[i:i + self.n - 1]), [seq[i + self.n - 1]])
+            return
+        for i in range(len(seq)):
+            for j in range(min(self.n - 1, i), 1, -1):
+                self._add(j, tuple(seq[i - j:i]), [seq[i]])
+
+
+def ngram_assisted_generate(inputs: List[int], store: NgramStore, target, gamma: int, filler_top_k: int,
+                            proc: Processor, max_gen_len: int, eos_tokens_id, pad_token_id: int = 0,
+                            first_target: bool = True, stop_if_unknown: bool = False,
+                            noise: Optional[TorchNoise] = None, exact: bool = False) -> Tuple[List[int], float]:
+    """ngram_assisted/ngram_assisted.py:11-164 (A11) restated: drafts from the n-gram store, the
+    sample-and-compare verify (n = first i whose sample of p_i differs from draft i), no residual,
+    a second independent draw from p_n (or the bonus row), the filler updates with topk(p)."""
+    noise = noise or store.noise
+    stops = eos_tokens_id if isinstance(eos_tokens_id, list) else [eos_tokens_id]
+    acc = spec = 0.0
+    P = len(inputs)
+    total = min(target.config.max_position_embeddings, P + max_gen_len)
+    ids = [pad_token_id] * total
+    ids[:P] = list(inputs)
+    cur = P
+    store.initialize(ids[:P])
+
+    def rate():
+        return acc / spec if spec > 0 else 0.0
+
+    def topk_ids(probs_row):
+        return probs_row.topk(filler_top_k).indices.tolist()
+
+    if first_target:                                                     # :78-93
+        logits = target(input_ids=torch.tensor([ids[:cur]])).logits
+        x = int(sample(process(logits[0, -1:, :], proc, exact), proc, noise).reshape(-1)[0])
+        ids[P] = x
+        cur += 1
+        store.update(ids[:P], [x])
+    while cur < total:                                                   # :95
+        g = min(gamma, total - cur - 1)
+        drafted = list(ids)
+        for k in range(g):                                               # :101-105
+            tok, known = store.next_token(drafted[:cur + k])
+            drafted[cur + k] = tok
+            if not known and stop_if_unknown:
+                g = k
+                break
+        spec += g
+        logits = target(input_ids=torch.tensor([drafted[:cur + g]])).logits[0]   # :111-115
+        p = process(logits[cur - 1:cur + g - 1], proc, exact)            # [g, V]
+        n = g
+        for i in range(g):                                               # :118-122
+            if int(sample(p[i], proc, noise).reshape(-1)[0]) != drafted[cur + i]:
+                n = i
+                break
+        acc += n
+        for j in range(n):                                               # :126-131
+            if drafted[cur + j] in stops:
+                return drafted[P:cur + j + 1], rate()
+        p_p = process(logits[cur + g - 1:cur + g], proc, exact)[0] if n == g else p[n]   # :134-143
+        x = int(sample(p_p, proc, noise).reshape(-1)[0])
+        ids[cur:cur + n] = drafted[cur:cur + n]
+        ids[cur + n] = x
+        for i in range(n):                                               # :151-155
+            store.update(ids[:cur + i], [ids[cur + i]])
+            if filler_top_k > 1:
+                store.update(ids[:cur + i], topk_ids(p[i]))
+        store.update(ids[:cur + n], [x])
+        if filler_top_k > 1:
+            store.update(ids[:cur + n], topk_ids(p_p))
+        cur += n + 1
+        if x in stops:                                                   # :161-164
+            return ids[P:cur], rate()
+    return ids[P:], rate()
+
+
 # --------------------------------------------------------------------------
 # KV-cache prune (utils/caching.py)
 # --------------------------------------------------------------------------

@@ -24,6 +24,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 #include "sd_device.h"
 
@@ -100,6 +101,12 @@ struct Plan {
     int32_t tails;        // perf mode: decide / finish in last-arrival tails (1) or own launches (0)
     int32_t coh;          // partials may come from the same launch: read them agent-coherently
     int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
+    int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
+    // sd_ngram_verify (sd_ngram.inc)
+    struct NgPart* ngpart;
+    int64_t* filler_ids;
+    int64_t filler_stride;
+    int32_t filler_k;
 };
 
 // Phase timestamps (diagnostic builds, -DSD_PHASE_TIMING): thread 0 of workgroup `wg` records
@@ -286,56 +293,85 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
     const RowKeep kp = has_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    const int64_t lo = (int64_t)chunk * P.chunk;
-    const int64_t hi = lo + P.chunk < P.V ? lo + P.chunk : P.V;
+    // This workgroup's stages (STEP elements each) of the row: interleaved (stage chunk + i * n_chunks,
+    // so concurrently running workgroups stream adjacent blocks) or one contiguous span.
+    const int nst = (P.V + STEP - 1) / STEP;
+    const int spw = P.chunk / STEP;
+    const bool ilv = P.stats_interleave != 0;
+    const int cnt = ilv ? (chunk < nst ? (nst - chunk + P.n_chunks - 1) / P.n_chunks : 0)
+                        : (chunk * spw < nst ? min(spw, nst - chunk * spw) : 0);
+    auto stage_of = [&](int i) -> int64_t { return ilv ? chunk + (int64_t)i * P.n_chunks : (int64_t)chunk * spw + i; };
+    const int64_t hi = P.V;
     const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-    const int nit = (int)((hi - lo + STEP - 1) / STEP);
+    // the row's last stage is partial when STEP does not divide V: it is this workgroup's last, if any
+    const bool last_partial = cnt > 0 && (stage_of(cnt - 1) + 1) * STEP > P.V;
     float m = -INFINITY, acc = 0.f;
 
     // Terms are exp(y - m) = exp2((y - m) * log2e): subtract, multiply, v_exp_f32.  y - m is exact
     // for bf16/fp16 values (and for fp32 ones within 2^24 of each other); the multiply's rounding
     // gives each term an independent ~|y-m|*6e-8 relative error that averages down in the sum, and
     // no rounded product is shared by all terms, so S carries no common bias.  Consumers compute
-    // numerators with the compensated sd_exp.  The running reference m may trail the true max by
-    // up to 20 (terms stay <= e^20): rescales become rare after the first vectors, and every
-    // consumer uses (m, S) as a pair.
-    auto consume = [&](const float* x, int64_t e0) {
+    // numerators with the compensated sd_exp and use (m, S) as a pair.
+    // The reference m is NOT kept at the running max (a per-element max and a per-vector branch
+    // on it cost ~25% of this pass): a vector is summed against the current m, and only when its
+    // sum is not below 2^64 — a term more than 44 e-folds above m, the first vector (m = -inf),
+    // or an inf / NaN — m is raised to the vector's max, the running sum rescaled and the vector
+    // re-summed.  So m may trail the true max by up to 44 and S stays far below fp32 overflow
+    // (at most 2^64 per element).  NaN propagates; vectors of -inf only add nothing.
+    // CHECKED: the vector may run past the span (ragged tail); full stages skip the bound checks
+    auto consume = [&](const float* x, int64_t e0, auto checked) {
         float y[VEC];
-        float vm = -INFINITY;
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
-            y[k] = (e0 + k < hi) ? (FAST ? x[k] : process_value<DT>(x[k], e0 + k, T, has_keep, kp)) : -INFINITY;
-            vm = fmaxf(vm, y[k]);
+            y[k] = FAST ? x[k] : process_value<DT>(x[k], e0 + k, T, has_keep, kp);
+            if constexpr (decltype(checked)::value) y[k] = e0 + k < hi ? y[k] : -INFINITY;
         }
-        if (vm > m + 20.f) {
-            acc = m > -INFINITY ? acc * sd_exp(m - vm) : 0.f;
-            m = vm;
-        }
-        if (m > -INFINITY) {
+        float sv = 0.f;
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) acc += __builtin_amdgcn_exp2f((y[k] - m) * kLog2e);
+        for (int k = 0; k < VEC; ++k) sv += __builtin_amdgcn_exp2f((y[k] - m) * kLog2e);
+        if (!(sv < 1.8446744e19f)) {   // 2^64 (rare)
+            float vm = -INFINITY;
+            bool nan = false;
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) {
+                vm = fmaxf(vm, y[k]);
+                nan |= y[k] != y[k];
+            }
+            if (vm > m) {
+                acc = m > -INFINITY ? acc * sd_exp(m - vm) : 0.f;
+                m = vm;
+            }
+            sv = 0.f;
+            if (m > -INFINITY) {
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) sv += __builtin_amdgcn_exp2f((y[k] - m) * kLog2e);
+            }
+            if (nan) {   // softmax of a row with a NaN is NaN: make it stick through every merge
+                sv = NAN;
+                if (!(m > -INFINITY)) m = 0.f;
+            }
         }
+        acc += sv;
     };
     // steady state: stages where every lane's 16-byte vector is in range.  Loads are issued
     // unconditionally (the prefetch index is clamped), so the compiler keeps kPipe of them in
     // flight with counted vmcnt waits instead of draining to vmcnt(0) each stage.
-    const int nfull = aligned ? (int)((hi - lo) / STEP) : 0;
+    const int nfull = aligned ? cnt - (last_partial ? 1 : 0) : 0;
     if (nfull > 0) {
-        const uint4* vb = reinterpret_cast<const uint4*>(static_cast<const char*>(row) + lo * Elem<DT>::kBytes) +
-                          threadIdx.x;
+        const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;   // stage k at vb[k * kThreads]
         uint4 buf[kPipe];
 #pragma unroll
-        for (int d = 0; d < kPipe; ++d) buf[d] = vb[(d < nfull ? d : nfull - 1) * kThreads];
+        for (int d = 0; d < kPipe; ++d) buf[d] = vb[stage_of(d < nfull ? d : nfull - 1) * kThreads];
         int it = 0;
         for (; it + kPipe <= nfull; it += kPipe) {
 #pragma unroll
             for (int d = 0; d < kPipe; ++d) {
                 const uint4 v = buf[d];
                 const int nx = it + d + kPipe;
-                buf[d] = vb[(nx < nfull ? nx : nfull - 1) * kThreads];
+                buf[d] = vb[stage_of(nx < nfull ? nx : nfull - 1) * kThreads];
                 float x[VEC];
                 unpack16<DT>(v, x);
-                consume(x, lo + ((int64_t)(it + d) * kThreads + threadIdx.x) * VEC);
+                consume(x, stage_of(it + d) * STEP + threadIdx.x * VEC, std::false_type{});
             }
         }
 #pragma unroll
@@ -343,17 +379,17 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
             if (it + d < nfull) {
                 float x[VEC];
                 unpack16<DT>(buf[d], x);
-                consume(x, lo + ((int64_t)(it + d) * kThreads + threadIdx.x) * VEC);
+                consume(x, stage_of(it + d) * STEP + threadIdx.x * VEC, std::false_type{});
             }
         }
     }
-    // ragged tail (and misaligned rows): guarded element loads
-    for (int it = nfull; it < nit; ++it) {
-        const int64_t e0 = lo + ((int64_t)it * kThreads + threadIdx.x) * VEC;
+    // the row's partial last stage (and misaligned rows): guarded element loads
+    for (int it = nfull; it < cnt; ++it) {
+        const int64_t e0 = stage_of(it) * STEP + threadIdx.x * VEC;
         float x[VEC];
 #pragma unroll
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < hi) ? load_one<DT>(row, e0 + k) : 0.f;
-        consume(x, e0);
+        consume(x, e0, std::true_type{});
     }
     float pf_xt = 0.f, pf_xd = 0.f;
     if (TAIL && threadIdx.x < P.gamma) fetch_drafted(P, b, threadIdx.x, pf_tok, &pf_xt, &pf_xd);
@@ -1486,6 +1522,8 @@ void set_stats_chunks(sd::Plan& P, int rows) {
     per_wg = per_wg < 1 ? 1 : (per_wg > 16 ? 16 : per_wg);
     P.chunk = (int32_t)(per_wg * stage);
     P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    P.stats_interleave = 0;   // measured: contiguous spans 38.4 us/step vs interleaved 39.2
+    if (const char* e = getenv("SD_STATS_INTERLEAVE")) P.stats_interleave = atoi(e);
 }
 
 // Resample / sample passes: 1 or 2 stages of 2048 elements per workgroup, about 1024 workgroups so
@@ -1786,3 +1824,5 @@ int32_t sd_probs(const sd_probs_args* a, void* stream) {
 }
 
 }  // extern "C"
+
+#include "sd_ngram.inc"

@@ -33,7 +33,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.g
 
 EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify_workspace_size", "sd_verify",
            "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",
-           "sd_mt19937_fill", "sd_mt19937_advance")
+           "sd_ngram_workspace_size", "sd_ngram_verify", "sd_mt19937_fill", "sd_mt19937_advance")
 
 
 class sd_processor(C.Structure):
@@ -85,6 +85,21 @@ class sd_probs_args(C.Structure):
     ]
 
 
+class sd_ngram_args(C.Structure):
+    _fields_ = [
+        ("batch", C.c_int32), ("gamma", C.c_int32), ("vocab", C.c_int32),
+        ("target_rows", C.c_void_p * (SD_MAX_GAMMA + 1)), ("target_stride_b", C.c_int64),
+        ("target_dtype", C.c_int32),
+        ("draft_tokens", C.c_void_p), ("draft_tokens_stride_b", C.c_int64),
+        ("proc", sd_processor), ("stop_tokens", C.c_void_p), ("n_stop", C.c_int32), ("filler_k", C.c_int32),
+        ("noise", sd_noise),
+        ("n_accepted", C.c_void_p), ("next_token", C.c_void_p), ("prune_target", C.c_void_p),
+        ("stop_index", C.c_void_p), ("row_status", C.c_void_p), ("words_used", C.c_void_p),
+        ("filler_ids", C.c_void_p), ("filler_stride_b", C.c_int64),
+        ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+    ]
+
+
 def _share_torch_hip_runtime():
     """Load PyTorch-ROCm's bundled HIP runtime first, so libspecdec.so (NEEDED libamdhip64.so.7,
     which that copy's SONAME satisfies) binds to the SAME runtime torch uses instead of loading
@@ -114,6 +129,10 @@ def _load():
     for ws in ("sd_verify_workspace_size",):
         getattr(lib, ws).restype = C.c_size_t
         getattr(lib, ws).argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    lib.sd_ngram_workspace_size.restype = C.c_size_t
+    lib.sd_ngram_workspace_size.argtypes = [C.c_int32, C.c_int32, C.c_int32]
+    lib.sd_ngram_verify.restype = C.c_int32
+    lib.sd_ngram_verify.argtypes = [C.POINTER(sd_ngram_args), C.c_void_p]
     for ws in ("sd_sample_workspace_size", "sd_probs_workspace_size"):
         getattr(lib, ws).restype = C.c_size_t
         getattr(lib, ws).argtypes = [C.c_int32, C.c_int32]

@@ -257,3 +257,75 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         noise.advance(int(out.words_used.item()))
     del keep
     return out
+
+
+# --------------------------------------------------------------------------- n-gram verify (A11)
+@dataclass
+class NgramOut:
+    n_accepted: torch.Tensor      # int32 [B]
+    next_token: torch.Tensor      # int64 [B] (-1: a stop token among the accepted drafts)
+    prune_target: torch.Tensor    # int32 [B]
+    stop_index: torch.Tensor      # int32 [B]
+    row_status: torch.Tensor      # int32 [B]
+    filler_ids: Optional[torch.Tensor]   # int64 [B, γ'+1, K]
+    words_used: torch.Tensor      # int64 [1]
+
+
+def ngram_verify(target_rows: Sequence[torch.Tensor], draft_tokens: Optional[torch.Tensor], proc, noise,
+                 stop_tokens: Optional[torch.Tensor] = None, filler_k: int = 0, sync_noise: bool = True,
+                 row_base: int = 0) -> NgramOut:
+    """ngram_assisted/ngram_assisted.py:111-164 verify step for B sequences.
+
+    target_rows: γ'+1 tensors [B, V] — rows 0..γ'-1 verify drafts 0..γ'-1, row γ' is the bonus row;
+    draft_tokens: int64 [B, >=γ'] (None when γ' == 0).  Under StreamNoise the torch generator
+    advances by the words the draws consumed (the reference's order), one device->host read."""
+    spec = proc_spec(proc)
+    gamma = len(target_rows) - 1
+    if not 0 <= gamma <= _lib.SD_MAX_GAMMA:
+        raise ValueError(f"gamma must be in [0, {_lib.SD_MAX_GAMMA}], got {gamma}")
+    if not 0 <= filler_k <= 8:
+        raise ValueError("filler_k must be in [0, 8]")
+    B, V = target_rows[0].shape
+    dev = target_rows[0].device
+    tdt = target_rows[0].dtype
+    t_stride = target_rows[0].stride(0) if B > 1 else 0
+    for i, t in enumerate(target_rows):
+        _require_rows(t, f"target_rows[{i}]", V)
+        if t.shape[0] != B or t.dtype != tdt or (B > 1 and t.stride(0) != t_stride):
+            raise ValueError("target rows must share batch, dtype and batch stride")
+    if gamma > 0:
+        if draft_tokens is None or draft_tokens.dtype != torch.long or draft_tokens.shape[0] != B \
+                or draft_tokens.shape[1] < gamma or draft_tokens.stride(1) != 1:
+            raise ValueError("draft_tokens must be int64 [B, >=gamma] with a contiguous last axis")
+        draft_tokens = draft_tokens.to(dev)
+    if stop_tokens is None:
+        stop_tokens = torch.empty(0, dtype=torch.long, device=dev)
+    stop_tokens = stop_tokens.to(device=dev, dtype=torch.long).contiguous()
+    i32 = dict(dtype=torch.int32, device=dev)
+    out = NgramOut(torch.empty(B, **i32), torch.empty(B, dtype=torch.long, device=dev), torch.empty(B, **i32),
+                   torch.empty(B, **i32), torch.empty(B, **i32),
+                   torch.empty(B, gamma + 1, filler_k, dtype=torch.long, device=dev) if filler_k else None,
+                   torch.empty(1, dtype=torch.long, device=dev))
+    need = B * (gamma + 1) * 2 * V if spec.stochastic else 0
+    nz, keep = _noise_struct(noise, need, dev, row_base)
+    ws = _workspace(lib.sd_ngram_workspace_size(B, gamma, V), dev)
+    a = _lib.sd_ngram_args()
+    a.batch, a.gamma, a.vocab = B, gamma, V
+    for i, t in enumerate(target_rows):
+        a.target_rows[i] = t.data_ptr()
+    a.target_stride_b, a.target_dtype = t_stride, _DT[tdt]
+    a.draft_tokens = draft_tokens.data_ptr() if gamma > 0 else None
+    a.draft_tokens_stride_b = draft_tokens.stride(0) if gamma > 0 else 0
+    a.proc, a.stop_tokens, a.n_stop, a.filler_k = spec.struct(), stop_tokens.data_ptr(), stop_tokens.numel(), filler_k
+    a.noise = nz
+    a.n_accepted, a.next_token = out.n_accepted.data_ptr(), out.next_token.data_ptr()
+    a.prune_target, a.stop_index = out.prune_target.data_ptr(), out.stop_index.data_ptr()
+    a.row_status, a.words_used = out.row_status.data_ptr(), out.words_used.data_ptr()
+    a.filler_ids = out.filler_ids.data_ptr() if filler_k else None
+    a.filler_stride_b = (gamma + 1) * filler_k
+    a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    _lib.check(lib.sd_ngram_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_ngram_verify")
+    if isinstance(noise, StreamNoise) and sync_noise:
+        noise.advance(int(out.words_used.item()))
+    del keep
+    return out

@@ -56,16 +56,22 @@ class FakeLM:
 
 
 def make_banks(vocab: int, rows: int = 64, sigma: float = 1.0, seed: int = 0,
-               scale: float = 3.0, dtype=torch.bfloat16):
+               scale: float = 3.0, dtype=torch.bfloat16, peak: float = 0.0):
+    """Target / drafter logit banks.  peak > 0 boosts one token per bank row by `peak` (a peaked,
+    LM-like distribution: sampled continuations repeat, so n-gram drafters get accepted)."""
     g = torch.Generator().manual_seed(seed)
     t = torch.randn(rows, vocab, generator=g) * scale
     d = t + sigma * torch.randn(rows, vocab, generator=g)
+    if peak > 0:
+        hot = torch.randint(0, vocab, (rows,), generator=torch.Generator().manual_seed(seed + 555))
+        t[torch.arange(rows), hot] += peak
+        d[torch.arange(rows), hot] += peak
     return t.to(dtype), d.to(dtype)
 
 
 def make_pair(vocab: int, rows: int = 64, sigma: float = 1.0, seed: int = 0, dtype=torch.bfloat16,
-              device="cpu", max_position_embeddings: int = 4096, pos_mult: int = 7):
-    t, d = make_banks(vocab, rows, sigma, seed, dtype=dtype)
+              device="cpu", max_position_embeddings: int = 4096, pos_mult: int = 7, peak: float = 0.0):
+    t, d = make_banks(vocab, rows, sigma, seed, dtype=dtype, peak=peak)
     return (FakeLM(t.to(device), max_position_embeddings, pos_mult),
             FakeLM(d.to(device), max_position_embeddings, pos_mult))
 

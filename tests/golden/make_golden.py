@@ -12,6 +12,7 @@ banks of tests/fakelm.py under fixed ``torch.manual_seed`` seeds, and writes:
 * ``engine_loops.json`` — ``engine.infer_engine.batch_speculative_generate`` outputs (rule A10)
 * ``processors.safetensors`` — ``utils.logits_processor`` probabilities on small rows
 * ``caching.json``      — ``utils.caching.prune_tuple_cache`` shapes
+* ``ngram_loops.json``  — ``ngram_assisted.ngram_assisted_speculative_generate`` outputs (rule A11)
 
 Only data is committed (inputs are regenerated from seeds + checked by digest);
 no reference source travels.  The GPU box never runs this script.
@@ -73,6 +74,23 @@ ENGINE_CASES = [
     ("llama_b2_g4_fp32", 128256, "fp32", 2, 4, 12, [128001, 128009], [0]),
 ]
 
+# ngram-assisted loop (rule A11): FakeLM target, the reference's n-gram storages as the drafter
+NGRAM_PEAK = 20.0
+NGRAM_CASES = [
+    # name, V, dtype, storage(kind, n), gamma, processor, filler_top_k, stop_if_unknown, gen_len, eos, seeds
+    ("ng_greedy_g4_n3", 4096, "bf16", ("multi", 3), 4, ("greedy", 1.0, 0, 1.0), 3, False, 48, [1], [0, 1]),
+    ("ng_greedy_g8_n4_f1", 4096, "bf16", ("multi", 4), 8, ("greedy", 1.0, 0, 1.0), 1, False, 48, [1], [0]),
+    ("ng_greedy_g4_one3_unknown", 4096, "bf16", ("one", 3), 4, ("greedy", 1.0, 0, 1.0), 3, True, 40, [1], [0, 1]),
+    ("ng_multi_g4_n3", 4096, "bf16", ("multi", 3), 4, ("multinomial", 1.0, 0, 1.0), 3, False, 40, [1], [0, 1, 2]),
+    ("ng_multi_t07_g8_n3", 4096, "bf16", ("multi", 3), 8, ("multinomial", 0.7, 0, 1.0), 3, False, 40, [1], [0]),
+    ("ng_nucleus09_g8_n3", 4096, "bf16", ("multi", 3), 8, ("nucleus", 1.0, 0, 0.9), 3, False, 40, [1], [0, 1]),
+    ("ng_topk20_g4_one3", 4096, "bf16", ("one", 3), 4, ("topk", 1.0, 20, 1.0), 3, False, 40, [1], [0]),
+    ("ng_greedy_g4_n3_eos", 4096, "bf16", ("multi", 3), 4, ("greedy", 1.0, 0, 1.0), 3, False, 60, "likely", [0, 1]),
+    ("ng_multi_g4_n3_fp32", 4096, "fp32", ("multi", 3), 4, ("multinomial", 1.0, 0, 1.0), 3, False, 40, [1], [0]),
+    ("ng_llama_nucleus_g8", 128256, "bf16", ("multi", 3), 8, ("nucleus", 1.0, 0, 0.9), 3, False, 24,
+     [128001, 128009], [0]),
+]
+
 DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
 
 
@@ -84,6 +102,12 @@ def _import_reference():
     from utils.caching import prune_tuple_cache                          # noqa
     from engine.infer_engine import batch_speculative_generate           # noqa
     return speculative_generate, lp, prune_tuple_cache, batch_speculative_generate
+
+
+def _import_reference_ngram():
+    _import_reference()
+    import ngram_assisted as ng                                          # noqa
+    return ng
 
 
 def prompt_for(V: int, seed: int, length: int = 8, batch: int = 1):
@@ -149,6 +173,31 @@ def main():
             print(name, seed, rec["raised"] or [len(o) for o in rec["outputs"]], flush=True)
     with open(os.path.join(HERE, "engine_loops.json"), "w") as f:
         json.dump(eng, f, indent=1)
+
+    ng = _import_reference_ngram()
+    ngl = {}
+    for name, V, dt, (skind, sn), gamma, (kind, T, k, p), filler, unknown, gen_len, eos, seeds in NGRAM_CASES:
+        # next-token logits depend on the last token only, peaked so sampled continuations repeat
+        target, _ = make_pair(V, dtype=DT[dt], pos_mult=0, peak=NGRAM_PEAK)
+        if eos == "likely":
+            eos = likely_tokens(target)
+        for seed in seeds:
+            prompt = prompt_for(V, seed, length=12)[0].tolist()
+            prompt = prompt + prompt[:6]   # a repeat so the storage starts with known grams
+            store = (ng.NGramStorage if skind == "multi" else ng.OneLevelNGramStorage)(sn, V)
+            torch.manual_seed(seed)
+            out, rate = ng.ngram_assisted_speculative_generate(
+                prompt, store, target, gamma=gamma, filler_top_k=filler,
+                logits_processor=make_processor(lp, kind, T, k, p), max_gen_len=gen_len,
+                eos_tokens_id=eos if len(eos) > 1 else eos[0], pad_token_id=0, stop_if_unknown=unknown)
+            ngl[f"{name}/s{seed}"] = dict(
+                vocab=V, dtype=dt, storage=skind, n=sn, gamma=gamma, pos_mult=0, peak=NGRAM_PEAK,
+                processor=dict(kind=kind, temperature=T, top_k=k, top_p=p), filler_top_k=filler,
+                stop_if_unknown=unknown, max_gen_len=gen_len, eos=eos, seed=seed, prompt=prompt,
+                target_digest=bank_digest(target), tokens=out, acceptance_rate=float(rate))
+            print(name, seed, len(out), rate, flush=True)
+    with open(os.path.join(HERE, "ngram_loops.json"), "w") as f:
+        json.dump(ngl, f, indent=1)
 
     # processors on small rows
     from safetensors.torch import save_file

@@ -470,3 +470,99 @@ def test_divergence_budget():
     print(f"[parity] torch-CPU rounding divergences: {len(DIVERGENCES)} {DIVERGENCES}")
     print(f"[parity] nucleus tie-order divergences: {len(TIE_DIVERGENCES)} {TIE_DIVERGENCES}")
     assert len(DIVERGENCES) <= 6
+
+
+# ---------------------------------------------------------------- n-gram verify (A11)
+NGRAM_STEP_GRID = [
+    # (g, V, dtype, kind, match drafts, stop at)
+    (4, 4096, torch.bfloat16, "greedy", 2, None),
+    (4, 4096, torch.bfloat16, "multi_t1", 3, None),
+    (8, 4096, torch.bfloat16, "nucleus09", 8, None),
+    (8, 4096, torch.bfloat16, "multi_t07", 1, None),
+    (4, 4096, torch.bfloat16, "topk20", 4, None),
+    (1, 4096, torch.float32, "multi_t1", 1, None),
+    (0, 4096, torch.bfloat16, "multi_t1", 0, None),
+    (4, 4096, torch.bfloat16, "greedy", 4, 1),
+    (4, 128256, torch.bfloat16, "multi_t1", 2, None),
+]
+
+
+@pytest.mark.parametrize("g,V,dtype,kind,match,stop_at", NGRAM_STEP_GRID)
+def test_ngram_verify_step_matches_oracle(sd, g, V, dtype, kind, match, stop_at):
+    proc = KINDS[kind]
+    seed = g * 31 + V % 97
+    x = rand_logits((g + 1, V), torch.float32, seed, 3.0)
+    hot = torch.randint(0, V, (g + 1,), generator=torch.Generator().manual_seed(seed + 1))
+    x[torch.arange(g + 1), hot] += 25.0            # peaked rows: samples equal the argmax almost surely
+    x = x.to(dtype)
+    drafts = [int(hot[i]) if i < match else (int(hot[i]) + 1) % V for i in range(g)]
+    stops = [drafts[stop_at]] if stop_at is not None else [3]
+    K = 3
+    variants = {}
+    for exact in (False, True):
+        gen = torch.Generator().manual_seed(5000 + seed)
+        noise = ref.TorchNoise(gen)
+        n, xo = ref.ngram_verify_step(x, drafts, proc, noise) if g > 0 else (0, None)
+        if g == 0:
+            xo = int(ref.sample(ref.process(x[0:1], proc, exact), proc, noise).reshape(-1)[0])
+        stop = next((j for j in range(n) if drafts[j] in stops), -1)
+        variants[exact] = (n, xo, stop, gen.get_state())
+    gen2 = torch.Generator().manual_seed(5000 + seed)
+    rows = [x[i:i + 1].to(DEV) for i in range(g + 1)]
+    dt = torch.tensor([drafts], dtype=torch.long, device=DEV) if g else None
+    out = sd.ops.ngram_verify(rows, dt, spec_of(sd, proc), sd.StreamNoise(gen2),
+                              torch.tensor(stops, dtype=torch.long, device=DEV), filler_k=K)
+    torch.cuda.synchronize()
+    n, xg, stop = int(out.n_accepted[0]), int(out.next_token[0]), int(out.stop_index[0])
+    ok = []
+    for exact, (n_o, x_o, stop_o, state) in variants.items():
+        # a stop among the accepted drafts returns before x is drawn: the oracle step drew x anyway
+        want = (n_o, -1 if stop_o >= 0 else x_o, stop_o)
+        if (n, xg, stop) == want:
+            ok.append(exact)
+            if stop_o < 0:
+                assert torch.equal(gen2.get_state(), state)
+    assert ok, ((n, xg, stop), variants)
+    # filler ids: the top-K processed probabilities of every row (equal values may come in any order)
+    p = ref.process(x, proc, True).float()
+    got = out.filler_ids[0].cpu()
+    for i in range(g + 1):
+        want_vals = p[i].topk(K).values
+        assert torch.equal(p[i][got[i]], want_vals), (i, got[i], p[i].topk(K))
+
+
+with open(os.path.join(os.path.dirname(__file__), "golden", "ngram_loops.json")) as f:
+    NGRAM_GOLDEN = json.load(f)
+
+
+@pytest.mark.parametrize("case", sorted(NGRAM_GOLDEN))
+def test_ngram_loop_matches_reference(sd, case):
+    from specdec_amd.ngram_assisted import NGramStorage, OneLevelNGramStorage, ngram_assisted_speculative_generate
+    from specdec_amd.utils.logits_processor import (GreedyProcessor, MultinomialProcessor, NucleusProcessor,
+                                                    TopKProcessor)
+    c = NGRAM_GOLDEN[case]
+    DTm = {"bf16": torch.bfloat16, "fp32": torch.float32}
+    target, _ = make_pair(c["vocab"], dtype=DTm[c["dtype"]], device=DEV, pos_mult=c["pos_mult"], peak=c["peak"])
+    pp = c["processor"]
+    proc = {"greedy": lambda: GreedyProcessor(pp["temperature"]),
+            "multinomial": lambda: MultinomialProcessor(pp["temperature"]),
+            "topk": lambda: TopKProcessor(pp["temperature"], pp["top_k"]),
+            "nucleus": lambda: NucleusProcessor(pp["temperature"], pp["top_p"])}[pp["kind"]]()
+    store = (NGramStorage if c["storage"] == "multi" else OneLevelNGramStorage)(c["n"], c["vocab"])
+    eos = c["eos"] if len(c["eos"]) > 1 else c["eos"][0]
+    torch.manual_seed(c["seed"])
+    out, rate = ngram_assisted_speculative_generate(c["prompt"], store, target, gamma=c["gamma"],
+                                                    filler_top_k=c["filler_top_k"], logits_processor=proc,
+                                                    max_gen_len=c["max_gen_len"], eos_tokens_id=eos,
+                                                    stop_if_unknown=c["stop_if_unknown"])
+    if out != c["tokens"] or rate != c["acceptance_rate"]:
+        # a torch-CPU rounding flip: then the exact-arithmetic oracle must agree
+        cpu_target, _ = make_pair(c["vocab"], dtype=DTm[c["dtype"]], pos_mult=c["pos_mult"], peak=c["peak"])
+        kp = ref.Processor(pp["kind"], pp["temperature"], pp["top_k"], pp["top_p"], stable_ties=True)
+        torch.manual_seed(c["seed"])
+        noise = ref.TorchNoise(None)
+        st = ref.NgramStore(c["storage"], c["n"], c["vocab"], noise)
+        want = ref.ngram_assisted_generate(c["prompt"], st, cpu_target, c["gamma"], c["filler_top_k"], kp,
+                                           c["max_gen_len"], eos, 0, True, c["stop_if_unknown"], noise, exact=True)
+        assert (out, rate) == want
+        note_divergence("exact", f"ngram loop {case}")

@@ -39,11 +39,14 @@ int main(void) {
   printf("sd_sample_args %zu\n", sizeof(sd_sample_args));
   printf("sd_probs_args %zu\n", sizeof(sd_probs_args));
   printf("sd_noise %zu\n", sizeof(sd_noise));
+  printf("sd_ngram_args %zu\n", sizeof(sd_ngram_args));
   F(sd_verify_args, draft_rows) F(sd_verify_args, draft_tokens) F(sd_verify_args, target_proc)
   F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
   F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end)
   F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes)
   F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes) F(sd_noise, row_base)
+  F(sd_ngram_args, target_rows) F(sd_ngram_args, draft_tokens) F(sd_ngram_args, proc) F(sd_ngram_args, noise)
+  F(sd_ngram_args, filler_ids) F(sd_ngram_args, workspace_bytes)
   return 0;
 }
 """
@@ -58,7 +61,8 @@ def test_ctypes_layout_matches_c_header():
         out = subprocess.check_output([exe]).decode().split("\n")
     got = dict(line.rsplit(" ", 1) for line in out if line)
     for name, cls in [("sd_verify_args", _lib.sd_verify_args), ("sd_sample_args", _lib.sd_sample_args),
-                      ("sd_probs_args", _lib.sd_probs_args), ("sd_noise", _lib.sd_noise)]:
+                      ("sd_probs_args", _lib.sd_probs_args), ("sd_noise", _lib.sd_noise),
+                      ("sd_ngram_args", _lib.sd_ngram_args)]:
         assert int(got[name]) == C.sizeof(cls), name
     for key, val in got.items():
         if "." in key:

@@ -16,6 +16,8 @@ with open(os.path.join(GOLD, "spec_loops.json")) as f:
     SPEC = json.load(f)
 with open(os.path.join(GOLD, "engine_loops.json")) as f:
     ENGINE = json.load(f)
+with open(os.path.join(GOLD, "ngram_loops.json")) as f:
+    NGRAM = json.load(f)
 
 _pairs = {}
 
@@ -41,6 +43,24 @@ def test_spec_loop_matches_reference(case):
                                          skip_sample_adjustment=c["skip_sample_adjustment"])
     assert out == c["tokens"]
     assert rate == pytest.approx(c["acceptance_rate"], abs=0, rel=0)
+
+
+@pytest.mark.parametrize("case", sorted(NGRAM))
+def test_ngram_loop_matches_reference(case):
+    """ngram_assisted_speculative_generate (A11) restated, against the reference's own outputs."""
+    c = NGRAM[case]
+    target, _ = make_pair(c["vocab"], dtype=DT[c["dtype"]], pos_mult=c["pos_mult"], peak=c["peak"])
+    assert bank_digest(target) == c["target_digest"]
+    pp = c["processor"]
+    proc = ref.Processor(pp["kind"], pp["temperature"], pp["top_k"], pp["top_p"])
+    eos = c["eos"] if len(c["eos"]) > 1 else c["eos"][0]
+    torch.manual_seed(c["seed"])
+    noise = ref.TorchNoise(None)
+    store = ref.NgramStore(c["storage"], c["n"], c["vocab"], noise)
+    out, rate = ref.ngram_assisted_generate(c["prompt"], store, target, c["gamma"], c["filler_top_k"], proc,
+                                            c["max_gen_len"], eos, 0, True, c["stop_if_unknown"], noise)
+    assert out == c["tokens"]
+    assert rate == c["acceptance_rate"]
 
 
 @pytest.mark.parametrize("case", sorted(ENGINE))
