@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 2
+#define SD_ABI_VERSION 3
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -160,9 +160,13 @@ typedef struct {
     size_t workspace_bytes;
 
     /* optional instrumentation: hipEvent_t recorded on `stream` right before / after the
-       row-statistics kernel (the pass that reads every logit row once); nullable.          */
+       row-statistics kernel (the pass that reads every logit row once); nullable.  With the
+       events set, the kernel is launched prof_stats_repeat (>= 1) times between them, back to
+       back (every repeat rewrites the same partials and decisions), so the event pair's own
+       cost is amortised over the repeats.                                                   */
     void* prof_stats_begin;
     void* prof_stats_end;
+    int32_t prof_stats_repeat;
 } sd_verify_args;
 
 typedef struct {

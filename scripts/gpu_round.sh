@@ -1,0 +1,18 @@
+#!/bin/bash
+# GPU-box recipe for the round's evidence: GPU tests, the default bench line (with the CPU
+# baseline), a rocprofv3 kernel-trace summary and the FETCH_SIZE / WRITE_SIZE PMC passes.
+# Outputs under gpurun_out/.
+set -eo pipefail
+R=$GRAFT_REPO_ROOT
+cd $R
+timeout -k 10 300 python -m pytest tests/test_gpu_perfmode.py -q -m gpu -x > gpurun_out/gpu_perf_tests.log 2>&1
+timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+export TMPDIR=/tmp
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- \
+  python3 $R/bench.py --steps 100 --no-cpu-baseline > $R/gpurun_out/prof.log 2>&1
+for c in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $R/gpurun_out/pmc_$c -o run -- \
+    python3 $R/bench.py --steps 20 --warmup 5 --prof-steps 5 --no-cpu-baseline > $R/gpurun_out/pmc_$c.log 2>&1
+done

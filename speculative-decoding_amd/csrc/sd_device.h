@@ -417,9 +417,10 @@ __device__ __forceinline__ uint4 philox_block(const sd_noise& nz, uint32_t row, 
     return philox4x32_10(c, make_uint2((uint32_t)nz.seed, (uint32_t)(nz.seed >> 32)));
 }
 
-// perf-mode U[0,1) at 53 bits for one inverse-CDF draw of row `row`
-__device__ __forceinline__ double cdf_uniform(const sd_noise& nz, uint32_t row) {
-    const uint4 q = philox_block(nz, row, kSiteCdf, 0u);
+// perf-mode U[0,1) at 53 bits for the inverse-CDF draws of row `row`: idx 0 picks the chunk,
+// idx 1 + c the element inside chunk c (independent blocks)
+__device__ __forceinline__ double cdf_uniform(const sd_noise& nz, uint32_t row, uint32_t idx = 0u) {
+    const uint4 q = philox_block(nz, row, kSiteCdf, idx);
     return (double)(((((uint64_t)q.x) << 32) | q.y) >> 11) * 1.1102230246251565e-16;   // 2^-53
 }
 

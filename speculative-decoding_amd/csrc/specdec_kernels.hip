@@ -48,8 +48,8 @@ struct ResPart {
     float sum;                 // Σ residual over the chunk
     float wmax;                // max residual / E
     int32_t ncand;             // candidates kept (> kMaxCand => overflow)
-    float pval;                // argmax value (bonus / p-row / engine p fallback)
-    int32_t pidx;
+    float pval;                // argmax value (bonus / p-row / engine p fallback); perf: Σ p
+    int32_t pidx;              // its index; perf stochastic: the chunk's own inverse-CDF pick
     float cres[kMaxCand];      // candidate residual value
     float ce[kMaxCand];        // candidate noise value
     int32_t cidx[kMaxCand];
@@ -1118,70 +1118,47 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
     }
 }
 
-// Inverse-CDF draw of sequence b (whole workgroup, after all chunk sums landed): a Philox U[0,1)
-// at 53 bits picks the chunk on the fp64 running sum of the chunk totals (lw: staged in LDS),
-// then the element on an fp64 prefix over the chunk's weights (recomputed bit-identically).
-// Every element's interval has its exact fp32 weight as width, so the draw is w_j / Σw up to the
-// rounding of the chunk totals (~1e-7 relative) — no per-element noise.  -1: no positive weight.
-template <int TDT, int DDT, bool FAST, int EPT>
-__device__ __forceinline__ int64_t cdf_pick(const Plan& P, const PairRows& R, int b, const float* lw, int wg_id) {
-    constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC, NW = kThreads / kWave;
-    __shared__ int s_chunk;
-    __shared__ double s_t;
+// Perf-mode sampling is a two-level inverse CDF.  Each sampling chunk c draws its own candidate
+// j_c with an independent Philox U'_c (chunk_pick, on the weights it holds in registers); the
+// sequence's tail then picks the chunk on the fp64 running sum of the chunk totals with U
+// (pick_chunk) and returns j_c.  P(c) = S_c / ΣS and P(j | c) = w_j / S_c, so the draw is w_j / Σw
+// up to the rounding of the chunk totals (~1e-7 relative), with no per-element noise and no
+// dependent reload of the chosen chunk.
+
+// The element of one chunk (whole workgroup; the thread's EPT weights in registers) whose interval
+// of the fp64 running sum in (thread, k) order holds u * total.  Every element's interval has its
+// exact fp32 weight as width.  Returns the position tid * EPT + k (uniform), -1 without positive
+// weight; total: the chunk's fp64 Σ weight, ptotal: the block sum of pextra (fixed order).
+template <int EPT>
+__device__ __forceinline__ int chunk_pick(const float* wv, double u, float pextra, double& total, float& ptotal) {
+    constexpr int NW = kThreads / kWave;
     __shared__ double s_wtot[NW];
+    __shared__ float s_ptot[NW];
     __shared__ int s_pos[NW], s_lastp[NW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    if (w == 0) {
-        // the chunk: first whose fp64 running total (chunk order) exceeds t = u * total
-        const double u = cdf_uniform(P.noise, (uint32_t)b);
-        int chunk = -1, lastpos = -1;
-        double excl = 0.0, t = 0.0;
-        double total = 0.0;
-        for (int c0 = 0; c0 < P.rn_chunks; c0 += kWave) {   // pass 1 (one group for V <= 128 Ki)
-            const float sv = c0 + lane < P.rn_chunks ? lw[c0 + lane] : 0.f;
-            total = lane_d(total + wave_incl_scan_d((double)sv), 63);
-        }
-        t = u * total;
-        double base = 0.0;
-        for (int c0 = 0; c0 < P.rn_chunks && chunk < 0; c0 += kWave) {
-            const float sv = c0 + lane < P.rn_chunks ? lw[c0 + lane] : 0.f;
-            const double incl = base + wave_incl_scan_d((double)sv);
-            const uint64_t hit = __ballot(incl > t && sv > 0.f);
-            const uint64_t pos = __ballot(sv > 0.f);
-            if (pos) lastpos = c0 + 63 - __builtin_clzll(pos);
-            if (hit) {
-                const int l = __builtin_ctzll(hit);
-                chunk = c0 + l;
-                excl = l > 0 ? lane_d(incl, l - 1) : base;
-            }
-            base = lane_d(incl, 63);
-        }
-        if (lane == 0) {
-            // rounding can leave t at/after the total: take the last positive chunk's end
-            s_chunk = chunk >= 0 ? chunk : lastpos;
-            s_t = chunk >= 0 ? t - excl : INFINITY;
-        }
-    }
-    __syncthreads();
-    SD_TS(wg_id, 7);
-    const int c = s_chunk;
-    if (c < 0) return -1;
-    const double t = s_t;
-    const int64_t base = (int64_t)c * P.rchunk;
-    float wv[EPT];
-#pragma unroll
-    for (int v = 0; v < NV; ++v) pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv + v * VEC);
     double tot = 0.0;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) tot += (double)wv[k];
-    SD_TS(wg_id, 8);
     // exclusive fp64 prefix of the thread totals in thread order: DPP scan, wave offsets via LDS
     const double wincl = wave_incl_scan_d(tot);
     double excl = dpp_d<0x138, 0xF, true>(0.0, wincl);   // wave_shr:1 -> the previous lane's inclusive
-    if (lane == 63) s_wtot[w] = wincl;
+    const float wp = wave_sum(pextra);
+    if (lane == 63) {
+        s_wtot[w] = wincl;
+        s_ptot[w] = wp;
+    }
     __syncthreads();
-    SD_TS(wg_id, 9);
-    for (int k = 0; k < w; ++k) excl += s_wtot[k];
+    double T = 0.0;
+    float PT = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        if (k < w) excl += s_wtot[k];
+        T += s_wtot[k];
+        PT += s_ptot[k];
+    }
+    total = T;
+    ptotal = PT;
+    const double t = u * T;
     // the thread whose interval [excl, excl + its weights) holds t finds the element
     int mypos = INT_MAX, lastp = -1;
     double run = excl;
@@ -1197,26 +1174,64 @@ __device__ __forceinline__ int64_t cdf_pick(const Plan& P, const PairRows& R, in
     if (lane == (hm ? __builtin_ctzll(hm) : 0)) s_pos[w] = hm ? mypos : INT_MAX;
     if (lane == (lm ? 63 - __builtin_clzll(lm) : 0)) s_lastp[w] = lm ? lastp : -1;
     __syncthreads();
-    SD_TS(wg_id, 10);
     int pos = INT_MAX, lp = -1;
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
         pos = s_pos[k] < pos ? s_pos[k] : pos;
         lp = s_lastp[k] > lp ? s_lastp[k] : lp;
     }
-    if (pos == INT_MAX) pos = lp;
-    if (pos < 0) return -1;
+    // rounding can leave t at/after the running total's end: the last positive element
+    return pos == INT_MAX ? lp : pos;
+}
+
+// vocabulary index of chunk_pick's position in the chunk starting at base
+template <int TDT, int DDT, int EPT>
+__device__ __forceinline__ int64_t chunk_elem(int64_t base, int pos) {
+    constexpr int VEC = PairVec<TDT, DDT>::kVec;
     const int tid = pos / EPT, k = pos - tid * EPT, v = k / VEC;
     return base + ((int64_t)v * kThreads + tid) * VEC + (k - v * VEC);
 }
 
-// Token of sequence b once every chunk partial has landed (whole workgroup): inverse CDF for
-// stochastic rows, the exact argmax-candidate pick for greedy ones; then the outputs and the
-// engine state.  A short chain of memory round trips: engine-state read issued first, all chunk
-// partials staged into LDS in one cooperative load, then the chosen chunk's rows.
+// The chunk of sequence b (whole workgroup; chunk totals lw staged in LDS): the first whose fp64
+// running total in chunk order exceeds U * Σ, U = Philox U[0,1) at 53 bits; -1: no positive total.
+__device__ __forceinline__ int pick_chunk(const Plan& P, int b, const float* lw) {
+    __shared__ int s_chunk;
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < kWave) {
+        const double u = cdf_uniform(P.noise, (uint32_t)b);
+        int chunk = -1, lastpos = -1;
+        double total = 0.0;
+        for (int c0 = 0; c0 < P.rn_chunks; c0 += kWave) {   // pass 1 (one group for V <= 128 Ki)
+            const float sv = c0 + lane < P.rn_chunks ? lw[c0 + lane] : 0.f;
+            total = lane_d(total + wave_incl_scan_d((double)sv), 63);
+        }
+        const double t = u * total;
+        double base = 0.0;
+        for (int c0 = 0; c0 < P.rn_chunks && chunk < 0; c0 += kWave) {
+            const float sv = c0 + lane < P.rn_chunks ? lw[c0 + lane] : 0.f;
+            const double incl = base + wave_incl_scan_d((double)sv);
+            const uint64_t hit = __ballot(incl > t && sv > 0.f);
+            const uint64_t pos = __ballot(sv > 0.f);
+            if (pos) lastpos = c0 + 63 - __builtin_clzll(pos);
+            if (hit) chunk = c0 + __builtin_ctzll(hit);
+            base = lane_d(incl, 63);
+        }
+        // rounding can leave t at/after the total: the last positive chunk
+        if (lane == 0) s_chunk = chunk >= 0 ? chunk : lastpos;
+    }
+    __syncthreads();
+    return s_chunk;
+}
+
+// Token of sequence b once every chunk partial has landed (whole workgroup): the chunk pick over
+// the staged chunk totals and that chunk's own candidate for stochastic rows, the exact
+// argmax-candidate pick for greedy ones; then the outputs and the engine state.  One memory round
+// trip: engine-state read issued first, every chunk partial staged into LDS in one cooperative
+// load.  Only the engine's den <= 1e-12 fallback re-reads a chunk (its p weights).
 template <int TDT, int DDT, bool FAST, bool STOCH>
 __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, int b, PairRows R, int wg_id) {
     constexpr int EPT = 8;
+    constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
     int64_t acc0 = 0;
     if (threadIdx.x == 0 && engine_state && (d.status & SD_ROW_DONE)) acc0 = P.accepted_count[b];   // early
@@ -1227,12 +1242,14 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
     int32_t status = d.status;
     if constexpr (STOCH) {
         __shared__ float l_sum[kTailChunks], l_pv[kTailChunks];
+        __shared__ int32_t l_cand[kTailChunks];
         __shared__ float s_mass;
         if (d.mode != kModeNone) {
             const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
             for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
                 l_sum[k] = ld_coh(&rp[k].sum);
                 l_pv[k] = ld_coh(&rp[k].pval);
+                l_cand[k] = ld_coh(&rp[k].pidx);
             }
             __syncthreads();
             if (threadIdx.x < kWave) {   // Σ residual, fixed order (lane-strided, then a butterfly)
@@ -1246,20 +1263,26 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
             SD_TS(wg_id, 4);
             // engine/infer_engine.py:319-321: den <= 1e-12 -> multinomial(p) over the target row
             const bool fallback = d.mode == kModeResid && P.rule == SD_RULE_ENGINE && (double)S <= 1e-12;
-            if (fallback) {
+            const int c = pick_chunk(P, b, fallback ? l_pv : l_sum);
+            SD_TS(wg_id, 7);
+            if (c >= 0 && !fallback) {
+                x = l_cand[c];
+            } else if (c >= 0) {
+                // the chosen chunk's p weights, re-read, and the same in-chunk draw as k_sample's
                 R.resid = false;   // same slot, same row stats: weights p
                 status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
+                const int64_t base = (int64_t)c * P.rchunk;
+                float wv[EPT];
+#pragma unroll
+                for (int v = 0; v < NV; ++v)
+                    pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv + v * VEC);
+                double T;
+                float PT;
+                const int pos = chunk_pick<EPT>(wv, cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c), 0.f, T, PT);
+                x = pos < 0 ? -1 : chunk_elem<TDT, DDT, EPT>(base, pos);
+            } else if (fallback) {
+                status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
             }
-#ifdef SD_CDF_TWICE   // diagnostic: the same code run twice (a real loop): warm vs cold instruction cache
-#pragma unroll 1
-            for (int rep = 0; rep < 2; ++rep) {
-                x = cdf_pick<TDT, DDT, FAST, EPT>(P, R, b, fallback ? l_pv : l_sum, wg_id);
-                if (rep == 0) SD_TS(wg_id, 11);
-                __syncthreads();
-            }
-#else
-            x = cdf_pick<TDT, DDT, FAST, EPT>(P, R, b, fallback ? l_pv : l_sum, wg_id);
-#endif
             SD_TS(wg_id, 5);
             if (d.mode == kModeResid) mass = S;
             if (x < 0) status |= SD_ROW_INVALID_DIST;   // no positive weight: torch.multinomial raises
@@ -1283,7 +1306,6 @@ template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL>
 __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_sample(Plan P) {
     constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
-    __shared__ float ldsf[8];
     const int wg_id = 8192 + blockIdx.y * gridDim.x + blockIdx.x;
     int b, c;
     if (P.xcd_affine) affine_split(wg_id - 8192, (int)gridDim.x, b, c);
@@ -1296,20 +1318,26 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
             // RESID also sums p: the engine's den <= 1e-12 fallback samples the target row itself
             R = pair_rows<TDT, DDT>(P, d, b);
             SD_TS(wg_id, 1);
-            float sum = 0.f, psum = 0.f;
+            // chunk Σ weight, Σ p, and the chunk's own inverse-CDF candidate (pick_chunk's comment)
+            const double u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
+            float psum = 0.f;
             const int64_t base = (int64_t)c * P.rchunk;
+            float wv[EPT];
 #pragma unroll
             for (int v = 0; v < NV; ++v) {
-                float wv[VEC], pv[VEC];
-                pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv, pv);
+                float pv[VEC];
+                pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv + v * VEC, pv);
 #pragma unroll
-                for (int k = 0; k < VEC; ++k) { sum += wv[k]; psum += pv[k]; }
+                for (int k = 0; k < VEC; ++k) psum += pv[k];
             }
-            const float2 bs = block_reduce2(make_float2(sum, psum), ldsf);
+            double T;
+            float PT;
+            const int pos = chunk_pick<EPT>(wv, u, psum, T, PT);
             if (threadIdx.x == 0) {
                 ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
-                st_coh(&o.sum, bs.x);
-                st_coh(&o.pval, bs.y);
+                st_coh(&o.sum, (float)T);
+                st_coh(&o.pval, PT);
+                st_coh(&o.pidx, pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos));
             }
         } else {
             const float2 mst = P.rowstat[b * P.slots + d.slot];
@@ -1741,7 +1769,9 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.xcd_affine = perf && P.B % 8 == 0;
     if (const char* e = getenv("SD_XCD_AFFINE")) P.xcd_affine = P.xcd_affine && atoi(e);
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
-    if (int32_t st = launch_stats(P, stream, perf && P.tails)) return st;
+    const int reps = a->prof_stats_begin && a->prof_stats_repeat > 1 ? a->prof_stats_repeat : 1;
+    for (int rep = 0; rep < reps; ++rep)
+        if (int32_t st = launch_stats(P, stream, perf && P.tails)) return st;
     if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
     if (perf && !P.tails) SD_LAUNCH(k_decide_perf, dim3(P.B), dim3(kThreads), stream, P);
     if (!perf) {   // parity mode: the reference's serial noise order

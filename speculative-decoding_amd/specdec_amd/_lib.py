@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 2
+SD_ABI_VERSION = 3
 SD_MAX_GAMMA = 16
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
@@ -63,7 +63,7 @@ class sd_verify_args(C.Structure):
         ("generated", C.c_void_p), ("generated_stride_b", C.c_int64), ("step", C.c_int32),
         ("finished", C.c_void_p), ("accepted_count", C.c_void_p),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
-        ("prof_stats_begin", C.c_void_p), ("prof_stats_end", C.c_void_p),
+        ("prof_stats_begin", C.c_void_p), ("prof_stats_end", C.c_void_p), ("prof_stats_repeat", C.c_int32),
     ]
 
 

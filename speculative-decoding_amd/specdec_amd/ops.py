@@ -250,8 +250,9 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         a.generated, a.generated_stride_b, a.step = gen.data_ptr(), gen.stride(0), int(engine_state["step"])
         a.finished, a.accepted_count = fin.data_ptr(), acc.data_ptr()
     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
-    if prof_events is not None:   # (torch.cuda.Event, torch.cuda.Event) around the row-stats kernel
+    if prof_events is not None:   # (torch.cuda.Event, torch.cuda.Event[, repeats]) around the row-stats kernel
         a.prof_stats_begin, a.prof_stats_end = prof_events[0].cuda_event, prof_events[1].cuda_event
+        a.prof_stats_repeat = int(prof_events[2]) if len(prof_events) > 2 else 1
     _lib.check(lib.sd_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_verify")
     if isinstance(noise, StreamNoise) and sync_noise:
         noise.advance(int(out.words_used.item()))

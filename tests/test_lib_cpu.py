@@ -42,7 +42,7 @@ int main(void) {
   printf("sd_ngram_args %zu\n", sizeof(sd_ngram_args));
   F(sd_verify_args, draft_rows) F(sd_verify_args, draft_tokens) F(sd_verify_args, target_proc)
   F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
-  F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end)
+  F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end) F(sd_verify_args, prof_stats_repeat)
   F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes)
   F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes) F(sd_noise, row_base)
   F(sd_ngram_args, target_rows) F(sd_ngram_args, draft_tokens) F(sd_ngram_args, proc) F(sd_ngram_args, noise)
