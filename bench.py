@@ -1,13 +1,15 @@
 #!/usr/bin/env python3
 """bench.py — throughput of the speculative verify/accept hot path on MI355X.
 
-Workload (BASELINE.json configs[2], per GPU): one verify step of the batched engine
-(engine/infer_engine.py:265-336, rule A10) over synthetic Llama-3 shaped logits resident in
-HBM — target [B, γ, V] and drafter [B, γ, V] bf16, B = 32 rows per GPU, γ = 4, V = 128256 —
-with draft tokens sampled from the drafter distribution.  A "step" is one sd_verify call:
-softmax statistics of all 2γ rows, the fp64 accept test, the (p−q)⁺ residual resample and
-the per-row outputs.  Independent prompt batches shard data-parallel (one replica per GPU, no
-collective on the data path), so scaling is weak: every rank verifies its own 32 rows.
+Workload (BASELINE.json configs[2], per GPU): the sampling hot path of one step of the batched
+engine (engine/infer_engine.py:238-336, rule A10) over synthetic Llama-3 shaped logits resident
+in HBM — target [B, γ, V] and drafter [B, γ, V] bf16, B = 32 rows per GPU, γ = 4, V = 128256.
+A "step" is γ drafter draws (softmax + multinomial of each [B, V] drafter row, :241-247, one
+sd_sample launch each, which also return the rows' softmax statistics) and one sd_verify call
+(softmax statistics of the γ target rows, the fp64 accept test, the (p−q)⁺ residual resample
+and the per-row outputs).  Every logit row is read once by the step, plus the two rows the
+residual samples from.  Independent prompt batches shard data-parallel (one replica per GPU,
+no collective on the data path), so scaling is weak: every rank verifies its own 32 rows.
 
 value = output tokens (accepted drafts + resampled tokens, all ranks) / max-over-ranks wall
 time of the K timed steps.  Steps run as hipGraph replays (the step is captured once per
@@ -89,16 +91,25 @@ def main():
     dl = (tl.float() + args.sigma * torch.randn(B, g, V, generator=gen, device=dev)).to(torch.bfloat16)
     noise = PhiloxNoise(seed=4242)
     draft = torch.empty(B, g, dtype=torch.long, device=dev)
-    for d in range(g):   # draft ids drawn from the drafter distribution (untimed setup)
-        tok, _, _ = ops.sample_rows(dl[:, d, :], ops.PLAIN_SOFTMAX, noise, row_base=row0)
-        draft[:, d] = tok
+    dstats = torch.empty(g, B, 2, dtype=torch.float32, device=dev)   # drafter rows' (max, Σexp)
     stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
     trows = [tl[:, t, :] for t in range(g)]
     drows = [dl[:, t, :] for t in range(g)]
 
-    def step(prof=None):
+    def draws():
+        # engine/infer_engine.py:241-247: softmax + multinomial of each drafter row, one launch per
+        # draft position (in the engine a drafter forward sits between them)
+        for d in range(g):
+            ops.sample_rows(drows[d], ops.PLAIN_SOFTMAX, noise, tokens_out=draft[:, d], row_base=row0,
+                            row_stats_out=dstats[d])
+
+    def verify(prof=None):
         return ops.verify(trows, drows, draft, _lib.SD_RULE_ENGINE, ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise,
-                          stops, prof_events=prof, row_base=row0)
+                          stops, prof_events=prof, row_base=row0, draft_row_stats=dstats)
+
+    def step(prof=None):
+        draws()
+        return verify(prof)
 
     for _ in range(max(args.warmup, 1)):
         step()
@@ -128,6 +139,19 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
+    # the verify alone (same captured draws' outputs), for the per-phase breakdown
+    vgraph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(vgraph):
+        for _ in range(G):
+            verify()
+    vgraph.replay()
+    torch.cuda.synchronize()
+    tv = time.perf_counter()
+    for _ in range(replays):
+        vgraph.replay()
+    torch.cuda.synchronize()
+    verify_ms = (time.perf_counter() - tv) / args.steps * 1e3
+
     # output tokens per replay (identical every replay: same inputs, same captured noise offsets)
     acc = sum(int(o.n_accepted.sum()) for o in outs)
     resid = sum(int(((o.row_status & _lib.SD_ROW_RESIDUAL) != 0).sum()) for o in outs)
@@ -136,7 +160,7 @@ def main():
     elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens, "accepted": acc * replays, "drafted": drafted}, dev, dist)
     tokens, accepted, drafted = tot["tokens"], tot["accepted"], tot["drafted"]
 
-    # dominant kernel: row statistics (reads every logit row once).  HIP events on its stream
+    # dominant kernel: row statistics of the target rows.  HIP events on its stream
     # around PROF_REPEAT back-to-back launches of it (sd_verify's prof_stats_repeat), so the
     # event pair's own cost (~3-6 us, context dependent) is amortised; the per-launch figure
     # still includes the launch-to-launch gaps, i.e. it errs on the slow side of rocprofv3's
@@ -145,14 +169,14 @@ def main():
     for e in ev:
         e[0].record()   # marks the torch events as recorded; sd_verify re-records them around k_stats
         e[1].record()
-        step(prof=(e[0], e[1], PROF_REPEAT))
+        verify(prof=(e[0], e[1], PROF_REPEAT))
     torch.cuda.synchronize()
     stats_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev) / PROF_REPEAT
-    rows_per_seq = 2 * g
-    alg_bytes = B * rows_per_seq * V * 2
+    alg_bytes = B * g * V * 2               # k_stats: the γ target rows, once
     achieved = alg_bytes / (stats_ms * 1e-3) / 1e9
     ms_per_step = elapsed / args.steps * 1e3
-    step_gbs = alg_bytes / (ms_per_step * 1e-3) / 1e9
+    step_bytes = B * 2 * g * V * 2          # the step: every target and drafter row once
+    step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -164,7 +188,7 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 rec = json.load(f)
-            key = f"engine_b{B}_g{g}_v{V}"
+            key = f"engine_drawstats_b{B}_g{g}_v{V}"
             if key in rec:
                 traffic = rec[key]["hbm_bytes_per_launch"]
         line = {
@@ -180,7 +204,8 @@ def main():
             "vs_baseline": None,
             "dtype": "bf16",
             "data": "synthetic (target logits ~ N(0,3^2), drafter = target + N(0,1), draft ids sampled from the drafter)",
-            "config": {"workload": "configs[2]: Llama-3-8B/3.2-1B logit shapes, engine verify step (rule A10)",
+            "config": {"workload": "configs[2]: Llama-3-8B/3.2-1B logit shapes, engine step sampling path: "
+                                   "γ drafter draws + verify (rule A10)",
                        "rows_per_gpu": args.batch, "global_batch": args.batch * world, "gamma": g, "vocab": V,
                        "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G},
             "acceptance_rate": accepted / drafted,
@@ -188,7 +213,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "k_stats", "kernel_ms": stats_ms, "launches_per_event_pair": PROF_REPEAT,
                          "alg_bytes_per_launch": alg_bytes,
-                         "step_achieved_gbs": step_gbs, "step_frac": step_gbs / HBM_PEAK_GBS},
+                         "step_bytes": step_bytes, "step_achieved_gbs": step_gbs,
+                         "step_frac": step_gbs / HBM_PEAK_GBS},
+            "phases_ms": {"draws": ms_per_step - verify_ms, "verify": verify_ms},
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -197,20 +224,24 @@ def main():
 
 
 def cpu_baseline(tl, dl, draft, args):
-    """Oracle (reference semantics, torch-CPU) on the same logits: softmax of the target and
-    drafter rows + the per-row accept/resample loop of engine/infer_engine.py:276-336."""
+    """Oracle (reference semantics, torch-CPU) on the same logits: the drafter draws
+    (softmax + multinomial per draft position, engine/infer_engine.py:241-247), the target
+    softmax and the per-row accept/resample loop of :276-336."""
     sys.path.insert(0, ROOT)
     from oracle import specdec_ref as ref
     cores = min(len(os.sched_getaffinity(0)), 16)
     torch.set_num_threads(cores)
     tlc, dlc, dc = tl.cpu(), dl.cpu(), draft.cpu()
     B, g, V = tlc.shape
-    noise = ref.TorchNoise(torch.Generator().manual_seed(0))
+    gen_cpu = torch.Generator().manual_seed(0)
+    noise = ref.TorchNoise(gen_cpu)
     t0 = time.perf_counter()
     steps = tokens = 0
     while True:
-        p = torch.softmax(tlc, dim=-1)
         q = torch.softmax(dlc, dim=-1).float()
+        for d in range(g):
+            dc[:, d] = torch.multinomial(q[:, d], 1, generator=gen_cpu).squeeze(-1)
+        p = torch.softmax(tlc, dim=-1)
         gen = torch.zeros(B, g, dtype=torch.long)
         gen[:, :] = dc
         fin = torch.zeros(B, dtype=torch.bool)
@@ -222,7 +253,8 @@ def cpu_baseline(tl, dl, draft, args):
             break
     dt = time.perf_counter() - t0
     return {"value": tokens / dt, "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": f"{steps} engine verify steps of the same {B}x{g}x{V} bf16 logits (oracle, torch-CPU)",
+            "sample": f"{steps} engine steps (γ drafter draws + verify) of the same {B}x{g}x{V} bf16 logits "
+                      "(oracle, torch-CPU)",
             "ms_per_step": dt / steps * 1e3}
 
 

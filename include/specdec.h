@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 3
+#define SD_ABI_VERSION 4
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -167,6 +167,16 @@ typedef struct {
     void* prof_stats_begin;
     void* prof_stats_end;
     int32_t prof_stats_repeat;
+
+    /* optional (nullable): (max, Σexp) of each processed drafter row as sd_sample returned it
+       with the draw (sd_sample_args.row_stats), pairs of floats; row d of sequence b at
+       draft_row_stats + 2 * (d * draft_row_stats_stride + b), stride >= batch.  With it the
+       row-statistics pass reads only the target rows — the drafter rows were read by their
+       draws (sampling/speculative_decoding.py:120-123, engine/infer_engine.py:241-247) — and
+       the residual still reads drafter row n.  A hint: ignored with draft_is_probs or a
+       top-k / nucleus drafter processor.                                                      */
+    const float* draft_row_stats;
+    int64_t draft_row_stats_stride;
 } sd_verify_args;
 
 typedef struct {
@@ -184,6 +194,10 @@ typedef struct {
     int64_t* words_used;         /* [1] (nullable)                                             */
     void* workspace;
     size_t workspace_bytes;
+    float* row_stats;            /* [R][2] (max, Σexp) of each processed row, the softmax
+                                    normaliser pair sd_verify takes as draft_row_stats (nullable).
+                                    PHILOX stochastic rows: ONE pass (k_draw) — each span draws
+                                    its own candidate, the row's last workgroup picks the span  */
 } sd_sample_args;
 
 /* LogitsProcessor.__call__ (utils/logits_processor.py:13-15) materialised: probs = softmax(_process(l)/T)

@@ -1,12 +1,14 @@
 #!/bin/bash
 # GPU-box recipe for the round's evidence: GPU tests, the default bench line (with the CPU
 # baseline), a rocprofv3 kernel-trace summary and the FETCH_SIZE / WRITE_SIZE PMC passes.
-# Outputs under gpurun_out/.
+# Outputs under gpurun_out/.  Every GPU step has its own time limit; the first failure ends it.
 set -eo pipefail
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 300 python -m pytest tests/test_gpu_perfmode.py -q -m gpu -x > gpurun_out/gpu_perf_tests.log 2>&1
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -q -m gpu -x > gpurun_out/gpu_tests.log 2>&1
+T="python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu"
+timeout -k 10 300 $T tests/test_gpu_draw.py > gpurun_out/gpu_draw_tests.log 2>&1
+timeout -k 10 300 $T tests/test_gpu_perfmode.py > gpurun_out/gpu_perf_tests.log 2>&1
+timeout -k 10 600 $T tests/test_gpu_parity.py > gpurun_out/gpu_tests.log 2>&1
 timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 export TMPDIR=/tmp
 cd /tmp

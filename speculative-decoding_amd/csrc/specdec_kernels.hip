@@ -82,6 +82,10 @@ struct Plan {
     int32_t* row_status;
     int64_t* words_used;
     float* token_prob;
+    float2* row_stats;          // sd_sample: (max, Σexp) of each processed row (nullable)
+    const float2* dstats;       // sd_verify: drafter row stats from sd_sample (nullable)
+    int64_t dstats_stride;      // element (d, b) at dstats[d * dstats_stride + b]
+    int32_t stat_slots;         // slots whose stats k_stats computes (the rest come from dstats)
     int64_t* generated;
     int64_t gen_stride;
     int32_t step;
@@ -413,7 +417,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     }
     if constexpr (TAIL) {
         __shared__ int s_last;
-        if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.slots * P.n_chunks));
+        if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.stat_slots * P.n_chunks));
         __syncthreads();
         SD_TS(wg_id, 2);
         if (s_last) {
@@ -460,6 +464,12 @@ __device__ __forceinline__ float prob_dyn(int dt, const void* row, int64_t j, fl
 // global memory after a barrier could hit a line another block on this CU cached earlier.
 __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    // drafter rows whose stats came with their draws (sd_sample row_stats): no partials
+    for (int s = P.stat_slots + (int)threadIdx.x; s < P.slots; s += (int)blockDim.x) {
+        const float2 ms = P.dstats[(int64_t)(s - P.n_tslots) * P.dstats_stride + b];
+        lstat[s] = ms;
+        if (publish) P.rowstat[b * P.slots + s] = ms;
+    }
     if (P.n_chunks <= kWave) {
         // one partial per lane per slot: issue every slot's load of this wave before reducing
         constexpr int kMaxSlotsPerWave = (2 * SD_MAX_GAMMA + 1 + 3) / 4;
@@ -467,13 +477,13 @@ __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
 #pragma unroll
         for (int k = 0; k < kMaxSlotsPerWave; ++k) {
             const int s = w + k * nw;
-            v[k] = (s < P.slots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
+            v[k] = (s < P.stat_slots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
                                                       : make_float2(-INFINITY, 0.f);
         }
 #pragma unroll
         for (int k = 0; k < kMaxSlotsPerWave; ++k) {
             const int s = w + k * nw;
-            if (s >= P.slots) break;
+            if (s >= P.stat_slots) break;
             const float m = wave_max(v[k].x);
             const float sum = wave_sum(v[k].x > -INFINITY ? v[k].y * sd_exp(v[k].x - m) : 0.f);
             if (lane == 0) {
@@ -483,7 +493,7 @@ __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
         }
         return;
     }
-    for (int s = w; s < P.slots; s += nw) {
+    for (int s = w; s < P.stat_slots; s += nw) {
         const float2 ms = combine_row(P, b * P.slots + s);
         if (lane == 0) {
             lstat[s] = ms;
@@ -1445,10 +1455,142 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
             const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
             P.token_prob[r] = (pi >= 0 && pi < P.V) ? prob_dyn(P.tdt, row, pi, P.tT, P.t_keep, kp, ms) : NAN;
         }
+        if (P.row_stats) P.row_stats[r] = ms;
         if (P.row_status) P.row_status[r] = st;
         if (r == 0 && P.words_used) *P.words_used = P.t_stoch ? 2ll * P.V * P.B : 0;
     }
 }
+
+// ------------------------------------------------------------------ k_draw (perf-mode sd_sample)
+// One launch, one pass over each row: LogitsProcessor.__call__ + MultinomialProcessor.sample
+// (utils/logits_processor.py:13-15,39-49) for PHILOX noise, plus the row's (max, Σexp) for the
+// verify step (sd_verify_args.draft_row_stats).  grid (span, R): a workgroup holds NST stages of
+// 2048 elements of row r in registers, takes their max m_c and weights w = exp(y - m_c), and
+// draws its own candidate j_c by inverse CDF with U'_c (chunk_pick); it publishes
+// (m_c, S_c, j_c, y_{j_c}).  The row's last arrival combines M = max m_c, S = Σ S_c·e^{m_c-M},
+// picks span c with probability S_c·e^{m_c-M} / S (U, pick_chunk) and returns j_c:
+// P(j) = e^{y_j-M} / S, the softmax of the processed row, with no second pass over it.
+// Greedy rows keep the exact two-pass argmax (rounded-probability ties need (M, S) first).
+template <int DT, bool FAST, int NST>
+__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_draw(Plan P) {
+    constexpr int VEC = Elem<DT>::kVec, STEP = kThreads * VEC, EPT = NST * VEC;
+    __shared__ float lm[kThreads / kWave];
+    const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
+    SD_TS(wg_id, 0);
+    int r, c;
+    if (P.xcd_affine) affine_split(wg_id, (int)gridDim.x, r, c);
+    else { r = blockIdx.y; c = blockIdx.x; }
+    const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
+    const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+    const RowKeep kp = (!FAST && P.t_keep) ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const int64_t base = (int64_t)c * NST * STEP;
+    float y[EPT];
+#pragma unroll
+    for (int v = 0; v < NST; ++v) {
+        const int64_t e0 = base + (int64_t)v * STEP + threadIdx.x * VEC;
+        float x[VEC];
+        load_vec<DT>(row, e0, P.V, al, x);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const float yk = FAST ? x[k] : process_value<DT>(x[k], e0 + k, P.tT, P.t_keep, kp);
+            y[v * VEC + k] = e0 + k < P.V ? yk : -INFINITY;
+        }
+    }
+    // span max (NaN sticks: fmaxf drops it, so track it apart)
+    float mv = -INFINITY;
+    bool nan = false;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        mv = fmaxf(mv, y[k]);
+        nan |= y[k] != y[k];
+    }
+    mv = wave_max(mv);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0) lm[w] = mv;
+    __syncthreads();
+    float m = lm[0];
+#pragma unroll
+    for (int k = 1; k < kThreads / kWave; ++k) m = fmaxf(m, lm[k]);
+    SD_TS(wg_id, 1);
+    float wv[EPT];
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) wv[k] = m > -INFINITY ? __builtin_amdgcn_exp2f((y[k] - m) * kLog2e) : 0.f;
+    double T;
+    float PT;
+    const int pos = chunk_pick<EPT>(wv, cdf_uniform(P.noise, (uint32_t)r, 1u + (uint32_t)c), nan ? 1.f : 0.f, T, PT);
+    SD_TS(wg_id, 2);
+    // the candidate's processed value, from the thread that holds it
+    __shared__ float s_ycand;
+    if (pos >= 0 && threadIdx.x == pos / EPT) {
+        const int k = pos - threadIdx.x * EPT;
+        float yc = y[0];
+#pragma unroll
+        for (int kk = 1; kk < EPT; ++kk) yc = kk == k ? y[kk] : yc;
+        s_ycand = yc;
+    }
+    __syncthreads();
+    // partial (m_c, S_c | j_c, y_{j_c}) as two 8-byte coherent stores into the span's 16-byte slot
+    float2* slot = reinterpret_cast<float2*>(reinterpret_cast<float4*>(P.rpart) + (int64_t)r * P.n_chunks + c);
+    if (threadIdx.x == 0) {
+        const float S = PT > 0.f ? NAN : (float)T;   // PT counts NaN lanes
+        st_coh(slot, make_float2(PT > 0.f && !(m > -INFINITY) ? 0.f : m, S));
+        st_coh(slot + 1, make_float2(__int_as_float(pos < 0 ? -1 : (int32_t)chunk_elem<DT, DT, EPT>(base, pos)),
+                                     pos < 0 ? -INFINITY : s_ycand));
+    }
+    __shared__ int s_last;
+    if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, r), (uint32_t)P.n_chunks);
+    __syncthreads();
+    SD_TS(wg_id, 3);
+    if (!s_last) return;
+
+    // ---- tail: the row's last arrival
+    __shared__ float l_w[kTailChunks], l_s[kTailChunks], l_y[kTailChunks];
+    __shared__ int32_t l_cand[kTailChunks];
+    __shared__ float2 s_ms;
+    {   // every span's partial in one staged round trip
+        const float2* pr = reinterpret_cast<const float2*>(reinterpret_cast<const float4*>(P.rpart) + (int64_t)r * P.n_chunks);
+        for (int k = threadIdx.x; k < P.n_chunks; k += kThreads) {
+            const float2 ms = ld_coh(pr + 2 * k), jy = ld_coh(pr + 2 * k + 1);
+            l_w[k] = ms.x;   // m_c for now; weights below
+            l_s[k] = ms.y;
+            l_cand[k] = __float_as_int(jy.x);
+            l_y[k] = jy.y;
+        }
+    }
+    __syncthreads();
+    SD_TS(wg_id, 4);
+    if (threadIdx.x < kWave) {
+        float M = -INFINITY;
+        for (int k = lane; k < P.n_chunks; k += kWave) M = fmaxf(M, l_w[k]);
+        M = wave_max(M);
+        float S = 0.f;
+        for (int k = lane; k < P.n_chunks; k += kWave) {
+            const float wc = l_w[k] > -INFINITY || l_s[k] != l_s[k] ? l_s[k] * sd_exp(l_w[k] - M) : 0.f;
+            l_w[k] = wc;
+            S += wc;
+        }
+        S = wave_sum(S);
+        if (lane == 0) s_ms = make_float2(M, S);
+    }
+    __syncthreads();
+    const float2 ms = s_ms;
+    const int cp = pick_chunk(P, r, l_w);
+    SD_TS(wg_id, 5);
+    if (threadIdx.x == 0) {
+        int32_t st = SD_ROW_DONE;
+        if (!(ms.y > 0.f) || ms.y != ms.y || ms.y == INFINITY) st |= SD_ROW_INVALID_DIST;   // torch raises
+        if (P.t_keep) st |= P.keep[r].flags;
+        const int64_t x = cp >= 0 ? (int64_t)l_cand[cp] : -1;
+        if (x < 0) st |= SD_ROW_INVALID_DIST;
+        P.next_token[r * P.next_token_stride] = x;
+        if (P.token_prob) P.token_prob[r] = x >= 0 ? prob_exact<DT>(l_y[cp], ms.x, ms.y, 1.0f / ms.y) : NAN;
+        if (P.row_stats) P.row_stats[r] = ms;
+        if (P.row_status) P.row_status[r] = st;
+        if (r == 0 && P.words_used) *P.words_used = 0;
+    }
+    SD_TS(wg_id, 6);
+}
+static_assert(sizeof(ResPart) >= sizeof(float4), "k_draw keeps a 16-byte partial per span in the ResPart region");
 
 // ------------------------------------------------------------------ sd_probs kernel
 template <int DT, int EPT>
@@ -1670,10 +1812,43 @@ int32_t launch_rowsample(const sd::Plan& P, void* stream) {
 // second launch starts after the first has finished, so the last arrival is always in it).
 int32_t launch_stats(const sd::Plan& P, void* stream, bool tail) {
     const bool t_fast = P.tT == 1.0f && !P.t_keep, d_fast = P.dT == 1.0f && !P.d_keep;
-    if (P.n_dslots == 0 || (P.tdt == P.ddt && t_fast == d_fast))
-        return launch_stats_group(P, P.tdt, t_fast, 0, P.slots, tail, stream);
+    const int d_cnt = P.stat_slots - P.n_tslots;   // drafter slots without stashed stats
+    if (d_cnt == 0 || (P.tdt == P.ddt && t_fast == d_fast))
+        return launch_stats_group(P, P.tdt, t_fast, 0, P.stat_slots, tail, stream);
     if (int32_t st = launch_stats_group(P, P.tdt, t_fast, 0, P.n_tslots, tail, stream)) return st;
-    return launch_stats_group(P, P.ddt, d_fast, P.n_tslots, P.n_dslots, tail, stream);
+    return launch_stats_group(P, P.ddt, d_fast, P.n_tslots, d_cnt, tail, stream);
+}
+
+// perf-mode sd_sample of stochastic rows: k_draw (one launch, one pass)
+template <int DT>
+int32_t launch_draw_dt(const sd::Plan& P, int nst, void* stream) {
+    const dim3 grid(P.n_chunks, P.B);
+    const bool fast = P.tT == 1.0f && !P.t_keep;
+    if (nst == 1) {
+        if (fast) SD_LAUNCH((k_draw<DT, true, 1>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_draw<DT, false, 1>), grid, dim3(kThreads), stream, P);
+    } else {
+        if (fast) SD_LAUNCH((k_draw<DT, true, 2>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_draw<DT, false, 2>), grid, dim3(kThreads), stream, P);
+    }
+    return SD_OK;
+}
+
+int32_t launch_draw(sd::Plan& P, void* stream) {
+    // spans of NST stages (2048 elements each): 1 while the grid fits one residency wave
+    const int64_t stage = kThreads * 8;
+    const int64_t nst_row = (P.V + stage - 1) / stage;
+    int nst = P.B * nst_row <= 2048 ? 1 : 2;
+    if (const char* e = getenv("SD_DRAW_STAGES")) nst = atoi(e) == 2 ? 2 : 1;
+    if (P.tdt == SD_F32) nst = 2;   // fp32 stages hold 1024 elements: keep spans >= 2048 (workspace sizing)
+    const int64_t step = kThreads * (int64_t)(P.tdt == SD_F32 ? 4 : 8);
+    P.chunk = (int32_t)(nst * step);
+    P.n_chunks = (int32_t)((P.V + P.chunk - 1) / P.chunk);
+    P.rn_chunks = P.n_chunks;   // pick_chunk's count
+    P.xcd_affine = P.B % 8 == 0;
+    if (P.tdt == SD_BF16) return launch_draw_dt<SD_BF16>(P, nst, stream);
+    if (P.tdt == SD_F32) return launch_draw_dt<SD_F32>(P, nst, stream);
+    return launch_draw_dt<SD_F16>(P, nst, stream);
 }
 
 }  // namespace
@@ -1729,6 +1904,7 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.n_tslots = n_t;
     P.n_dslots = a->draft_is_probs ? 0 : a->gamma;
     P.slots = P.n_tslots + P.n_dslots;
+    P.stat_slots = P.slots;
     P.tdt = a->target_dtype; P.ddt = a->draft_is_probs ? SD_F32 : a->draft_dtype;
     P.draft_is_probs = a->draft_is_probs; P.skip_adj = a->skip_sample_adjustment;
     P.t_keep = needs_keep(a->target_proc); P.d_keep = !a->draft_is_probs && needs_keep(a->draft_proc);
@@ -1747,6 +1923,14 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.stop_index = a->stop_index; P.row_status = a->row_status; P.words_used = a->words_used;
     P.generated = a->generated; P.gen_stride = a->generated_stride_b; P.step = a->step;
     P.finished = a->finished; P.accepted_count = a->accepted_count;
+    // drafter row stats that came with the draws (sd_sample row_stats): k_stats reads only the
+    // target rows.  A hint: ignored where the drafter rows carry a top-k / nucleus mask.
+    if (a->draft_row_stats && !a->draft_is_probs && !P.d_keep) {
+        if (a->draft_row_stats_stride < a->batch) return SD_ERR_INVALID;
+        P.dstats = reinterpret_cast<const float2*>(a->draft_row_stats);
+        P.dstats_stride = a->draft_row_stats_stride;
+        P.stat_slots = P.n_tslots;
+    }
 
     const int rows = P.B * P.slots;
     set_stats_chunks(P, rows);
@@ -1799,7 +1983,7 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     if (a->workspace_bytes < sd_sample_workspace_size(a->rows, a->vocab) || !a->workspace) return SD_ERR_WORKSPACE;
     Plan P{};
     P.B = a->rows; P.gamma = 1; P.V = a->vocab; P.rule = -1;
-    P.n_tslots = 1; P.n_dslots = 0; P.slots = 1;
+    P.n_tslots = 1; P.n_dslots = 0; P.slots = 1; P.stat_slots = 1;
     P.tdt = a->dtype; P.ddt = a->dtype;
     P.t_keep = needs_keep(a->proc); P.t_stoch = a->proc.kind != SD_PROC_GREEDY;
     P.tT = a->proc.temperature; P.dT = 1.f;
@@ -1807,12 +1991,20 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     P.noise = a->noise;
     P.next_token = a->tokens; P.next_token_stride = a->tokens_stride;
     P.token_prob = a->token_prob; P.row_status = a->row_status; P.words_used = a->words_used;
+    P.row_stats = reinterpret_cast<float2*>(a->row_stats);
     set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);
     if (P.t_keep) {
         const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
         if (st != SD_OK) return st;
+    }
+#ifdef SD_PHASE_TIMING
+    if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
+#endif
+    if (P.noise.mode == SD_NOISE_PHILOX && P.t_stoch) {
+        if (P.B > kCntMax || max_chunks(P.V) > kTailChunks) return SD_ERR_UNSUPPORTED;
+        return launch_draw(P, stream);   // one pass; the row's last arrival writes the outputs
     }
     set_rchunks(P);
     if (int32_t st = launch_stats(P, stream)) return st;
@@ -1830,7 +2022,7 @@ int32_t sd_probs(const sd_probs_args* a, void* stream) {
     if (a->workspace_bytes < sd_probs_workspace_size(a->rows, a->vocab) || !a->workspace) return SD_ERR_WORKSPACE;
     Plan P{};
     P.B = a->rows; P.gamma = 1; P.V = a->vocab; P.rule = -1;
-    P.n_tslots = 1; P.n_dslots = 0; P.slots = 1;
+    P.n_tslots = 1; P.n_dslots = 0; P.slots = 1; P.stat_slots = 1;
     P.tdt = a->dtype; P.ddt = a->dtype;
     P.t_keep = needs_keep(a->proc);
     P.tT = a->proc.temperature; P.dT = 1.f;

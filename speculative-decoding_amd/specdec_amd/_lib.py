@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 3
+SD_ABI_VERSION = 4
 SD_MAX_GAMMA = 16
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
@@ -64,6 +64,7 @@ class sd_verify_args(C.Structure):
         ("finished", C.c_void_p), ("accepted_count", C.c_void_p),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
         ("prof_stats_begin", C.c_void_p), ("prof_stats_end", C.c_void_p), ("prof_stats_repeat", C.c_int32),
+        ("draft_row_stats", C.c_void_p), ("draft_row_stats_stride", C.c_int64),
     ]
 
 
@@ -74,6 +75,7 @@ class sd_sample_args(C.Structure):
         ("tokens", C.c_void_p), ("tokens_stride", C.c_int64), ("token_prob", C.c_void_p),
         ("row_status", C.c_void_p), ("words_used", C.c_void_p),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+        ("row_stats", C.c_void_p),
     ]
 
 

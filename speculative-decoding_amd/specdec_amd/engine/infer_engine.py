@@ -23,7 +23,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import _lib
-from ..noise import default_noise
+from ..noise import PhiloxNoise, default_noise
 from ..ops import PLAIN_SOFTMAX, sample_rows, verify
 from .batch_decode import decode_batch_with_chat_template
 from .metrics import BatchMetrics, RequestMetrics
@@ -107,6 +107,9 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
     accepted = torch.zeros(B, dtype=torch.long, device=dev)
     stops = torch.tensor(list(ctx.end_tokens), dtype=torch.long, device=dev)
 
+    # perf mode: each draw also returns its row's (max, Σexp), so verify reads only target rows
+    stash = isinstance(noise, PhiloxNoise)
+    dstats = torch.empty(max(gamma, 1), B, 2, dtype=torch.float32, device=dev) if stash else None
     past = ctx.drafter(input_ids, attention_mask=attention_mask, use_cache=True).past_key_values   # :206
     step = 0
     while step < gen_len:                                                 # :211
@@ -124,7 +127,8 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
             out = ctx.drafter(prev.unsqueeze(1), past_key_values=past, use_cache=True)   # :239
             logits = out.logits[:, -1, :]
             past = out.past_key_values
-            samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise)     # :241-246 softmax + multinomial
+            samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise,     # :241-246 softmax + multinomial
+                                        row_stats_out=dstats[d] if stash else None)
             rows.append(logits)
             draft_tokens[:, d] = torch.where(active, samples, draft_tokens[:, d])          # :252
             generated[:, step + d] = torch.where(active, samples, generated[:, step + d])  # :257
@@ -140,7 +144,8 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
             rows = [r.to(t_logits.device) for r in rows]
         verify(trows, rows, draft_tokens, _lib.SD_RULE_ENGINE, PLAIN_SOFTMAX, PLAIN_SOFTMAX, noise, stops,
                active=active.to(torch.uint8),
-               engine_state=dict(generated=generated, step=step, finished=finished, accepted=accepted))
+               engine_state=dict(generated=generated, step=step, finished=finished, accepted=accepted),
+               draft_row_stats=dstats[:gw] if stash and t_logits.device == dev else None)
         step += gw                                                        # :338
 
     gen_host = generated.cpu()

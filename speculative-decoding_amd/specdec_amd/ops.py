@@ -101,11 +101,14 @@ def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
 
 # --------------------------------------------------------------------------- sampling
 def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Tensor] = None,
-                want_prob: bool = False, row_base: int = 0):
+                want_prob: bool = False, row_base: int = 0, row_stats_out: Optional[torch.Tensor] = None):
     """LogitsProcessor.__call__ + .sample on every row of logits [R, V] (one sample per row).
 
     Returns (tokens int64 [R], token_prob fp32 [R] or None, row_status int32 [R]).  Under
     StreamNoise the generator advances by 2·R·V words (torch.multinomial's Exp noise).
+    row_stats_out: optional fp32 [R, 2] device tensor (contiguous) that receives each processed
+    row's (max, Σexp) — what ``verify(draft_row_stats=...)`` takes so the verify step does not
+    re-read the drafter rows.  Under PhiloxNoise stochastic rows are drawn in ONE pass (k_draw).
     """
     spec = proc_spec(proc)
     R, V = logits.shape
@@ -116,6 +119,9 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
         raise ValueError("tokens_out must be an int64 device tensor with >= rows elements")
     prob = torch.empty(R, dtype=torch.float32, device=dev) if want_prob else None
     status = torch.empty(R, dtype=torch.int32, device=dev)
+    if row_stats_out is not None and (row_stats_out.dtype != torch.float32 or not row_stats_out.is_cuda
+                                      or row_stats_out.numel() < 2 * R or not row_stats_out.is_contiguous()):
+        raise ValueError("row_stats_out must be a contiguous fp32 device tensor with >= 2*rows elements")
     need = 2 * R * V if spec.stochastic else 0
     nz, keep = _noise_struct(noise, need, dev, row_base)
     nbytes = lib.sd_sample_workspace_size(R, V)
@@ -123,7 +129,8 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     a = _lib.sd_sample_args(R, V, logits.data_ptr(), logits.stride(0), _DT[logits.dtype], spec.struct(), nz,
                             tokens.data_ptr(), tokens.stride(0) if tokens.dim() == 1 else 1,
                             prob.data_ptr() if prob is not None else None, status.data_ptr(), None,
-                            ws.data_ptr(), ws.numel())
+                            ws.data_ptr(), ws.numel(),
+                            row_stats_out.data_ptr() if row_stats_out is not None else None)
     _lib.check(lib.sd_sample(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_sample")
     if isinstance(noise, StreamNoise):
         noise.advance(need)
@@ -165,7 +172,8 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
            rule: int, target_proc, draft_proc, noise, stop_tokens: Optional[torch.Tensor] = None,
            skip_sample_adjustment: bool = False, draft_is_probs: bool = False,
            active: Optional[torch.Tensor] = None, engine_state: Optional[dict] = None,
-           sync_noise: bool = True, prof_events=None, row_base: int = 0) -> VerifyOut:
+           sync_noise: bool = True, prof_events=None, row_base: int = 0,
+           draft_row_stats: Optional[torch.Tensor] = None) -> VerifyOut:
     """One verify step for B sequences.
 
     target_rows: γ+1 (SPEC) or γ (ENGINE) tensors [B, V] — row t of every sequence;
@@ -174,6 +182,9 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
     words the kernels consumed, which needs one device->host read (sync_noise).
     row_base: global row id of this call's row 0 under PhiloxNoise (data-parallel shards draw
     what one call over the whole batch would draw for the same rows).
+    draft_row_stats: optional fp32 [γ, B, 2] (or [γ, S>=B, 2]) device tensor — the drafter rows'
+    (max, Σexp) as ``sample_rows(row_stats_out=...)`` returned them with the draws; the
+    row-statistics pass then reads only the target rows.
     """
     gamma = len(draft_rows)
     if not 1 <= gamma <= _lib.SD_MAX_GAMMA:
@@ -207,6 +218,11 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         raise ValueError("stop_tokens must be an int64 device tensor")
     if active is not None and (active.dtype not in (torch.uint8, torch.bool) or active.numel() != B):
         raise ValueError("active must be uint8/bool [B]")
+    if draft_row_stats is not None:
+        ds = draft_row_stats
+        if ds.dtype != torch.float32 or ds.dim() != 3 or ds.shape[0] < gamma or ds.shape[1] < B \
+                or ds.shape[2] != 2 or ds.stride(2) != 1 or ds.stride(1) != 2 or ds.device != dev:
+            raise ValueError(f"draft_row_stats must be fp32 [>={gamma}, >={B}, 2] with (max, sum) pairs on {dev}")
 
     i32 = dict(dtype=torch.int32, device=dev)
     # every output is written by the kernels (no fill launches)
@@ -250,6 +266,8 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         a.generated, a.generated_stride_b, a.step = gen.data_ptr(), gen.stride(0), int(engine_state["step"])
         a.finished, a.accepted_count = fin.data_ptr(), acc.data_ptr()
     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    if draft_row_stats is not None:
+        a.draft_row_stats, a.draft_row_stats_stride = draft_row_stats.data_ptr(), draft_row_stats.stride(0) // 2
     if prof_events is not None:   # (torch.cuda.Event, torch.cuda.Event[, repeats]) around the row-stats kernel
         a.prof_stats_begin, a.prof_stats_end = prof_events[0].cuda_event, prof_events[1].cuda_event
         a.prof_stats_repeat = int(prof_events[2]) if len(prof_events) > 2 else 1
