@@ -24,12 +24,17 @@ tl = (torch.randn(B, G, V, device=dev, generator=g) * 3).to(torch.bfloat16)
 dl = (tl.float() + torch.randn(B, G, V, device=dev, generator=g)).to(torch.bfloat16)
 ids = dl.float().argmax(-1)
 noise = PhiloxNoise(seed=1)
+# the bench's verify: drafter rows' (max, Σexp) come from the draws, k_stats reads target rows only
+dstats = torch.empty(G, B, 2, device=dev)
+for d in range(G):
+    ops.sample_rows(dl[:, d], ops.PLAIN_SOFTMAX, noise, row_stats_out=dstats[d])
 ts = torch.zeros(16384 * 16, dtype=torch.int64, device=dev)
 
 
 def step():
     return ops.verify([tl[:, t] for t in range(G)], [dl[:, t] for t in range(G)], ids, _lib.SD_RULE_ENGINE,
-                      ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise, torch.tensor([], dtype=torch.long, device=dev))
+                      ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise, torch.tensor([], dtype=torch.long, device=dev),
+                      draft_row_stats=dstats)
 
 
 for _ in range(20):

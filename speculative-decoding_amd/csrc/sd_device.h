@@ -240,6 +240,15 @@ __device__ __forceinline__ float prob_exact(float y, float m, float S, float inv
     }
 }
 
+// Perf-mode sampling weight: the dtype-rounded probability from one exp2 and the reciprocal of S,
+// without prob_exact's correctly-rounded re-evaluation near a rounding boundary (fp32 error of a
+// few ulp: ~2e-4 of bf16 values land one ulp off, which moves a sampling weight by <= 2^-8 of
+// itself).  Decisions (p(x)/q(x)) and greedy picks keep prob_exact.
+template <int DT>
+__device__ __forceinline__ float prob_fast(float y, float m, float invS) {
+    return round_dt<DT>(__builtin_amdgcn_exp2f((y - m) * 1.44269502162933349609375f) * invS);
+}
+
 // ---------------------------------------------------------------- processors
 // Per-row keep predicate produced by the top-k / nucleus threshold search:
 // kept(j) <=> x_j > tau || (x_j == tau && j <= tie_idx).   tau=-inf, tie=INT_MAX keeps all.

@@ -167,6 +167,17 @@ __device__ __forceinline__ bool is_stop_l(const Plan& P, int64_t tok, const int6
     return false;
 }
 
+// SGPR budget of the streaming kernels: <= 80 keeps 8 workgroups of 256 threads resident per CU.
+// Overridable for tuning (-DSD_SGPR_CAP_N=n; 0 = the compiler's choice).
+#ifndef SD_SGPR_CAP_N
+#define SD_SGPR_CAP_N 80
+#endif
+#if SD_SGPR_CAP_N > 0
+#define SD_SGPR_CAP __attribute__((amdgpu_num_sgpr(SD_SGPR_CAP_N)))
+#else
+#define SD_SGPR_CAP
+#endif
+
 // ------------------------------------------------------------------ block helpers
 struct FMax {
     static constexpr float kId = -INFINITY;
@@ -218,7 +229,10 @@ __device__ __forceinline__ void block_argmax(float& v, int32_t& i, float* ldsv, 
 // grid (span, row-of-group): running max / Σexp of y = round_dt(_process(x)/T) over one span of a
 // row, streamed through a 4-deep register pipeline (16 B per lane per stage, 16 KiB per
 // workgroup in flight) with an online rescaled sum, so loads stay in flight while exp() runs.
-constexpr int kPipe = 4;
+#ifndef SD_STATS_PIPE
+#define SD_STATS_PIPE 4
+#endif
+constexpr int kPipe = SD_STATS_PIPE;
 constexpr float kLog2e = 1.44269502162933349609375f;
 
 __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
@@ -241,8 +255,45 @@ __device__ __forceinline__ const void* slot_row(const Plan& P, int b, int s) {
     return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
 }
 
-__device__ void decide_seq(const Plan& P, int b, int64_t pf_tok, float pf_xt, float pf_xd, int wg_id);
 __device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd);
+__device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64_t woff, bool* overrun);
+
+// What the perf-mode decision needs of draft i, gathered by one thread while the row statistics
+// stream: the drafted id and its accept uniform (prologue), its raw target / drafter logits, the
+// drafter row's (m, S) when they came with the draws, and its stop flag (after the stream).  Draft
+// i belongs to thread (i % nw) * 64 + i / nw — lane k of the wave that reduces target slot i in
+// seq_stats — so that wave can test draft i as soon as the slot's statistics are reduced.
+struct DraftPf {
+    int64_t tok = -1;
+    float xt = 0.f, xd = 0.f, u = 0.f;
+    float2 ds = make_float2(-INFINITY, 0.f);
+    bool stop = false;
+    bool act = true;   // engine rule: the sequence is active (draft 0's thread only)
+};
+__device__ __forceinline__ int pf_draft(const Plan& P) {
+    constexpr int nw = kThreads / kWave;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i = lane * nw + w;
+    return lane < (P.gamma + nw - 1) / nw && i < P.gamma ? i : -1;
+}
+__device__ __forceinline__ void pf_early(const Plan& P, int b, int i, DraftPf& pf) {
+    if (i >= 0) pf.tok = P.draft_tokens[b * P.tok_stride + i];
+}
+// after the stream: the loads go out together and the Philox ALU work runs while they (and the
+// workgroup's arrival) are in flight
+__device__ __forceinline__ void pf_late(const Plan& P, int b, int i, DraftPf& pf) {
+    if (i < 0) return;
+    fetch_drafted(P, b, i, pf.tok, &pf.xt, &pf.xd);
+    if (P.dstats) pf.ds = P.dstats[(int64_t)i * P.dstats_stride + b];
+    bool st = false;
+#pragma unroll 4
+    for (int k = 0; k < P.n_stop; ++k) st |= P.stops[k] == pf.tok;   // no early exit
+    pf.stop = st;
+    if (i == 0 && P.active) pf.act = P.active[b] != 0;
+    bool ovr = false;
+    pf.u = draw_uniform(P, b, i, 0, &ovr);   // perf mode: Philox, no stream words
+}
+__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id);
 
 // Arrival at a per-sequence counter (thread 0, after storing its partials with st_coh): true for
 // the last of `total` arrivals, which also re-arms the counter.  coh_wait() completes the
@@ -270,7 +321,7 @@ __device__ __forceinline__ void affine_split(int id, int per_seq, int& b, int& i
 // <= 80 SGPRs keeps 8 workgroups of 256 threads resident per CU (MI355X_MICROARCH.md, residency)
 // TAIL (perf mode): the last workgroup to finish a sequence's rows runs its decision (decide_seq).
 template <int DT, bool FAST, bool TAIL>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_stats(Plan P, int slot_lo, int slot_cnt) {
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot_lo, int slot_cnt) {
     __shared__ float lm[4], ls[4];
     constexpr int VEC = Elem<DT>::kVec;
     constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
@@ -291,8 +342,9 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     const void* row = slot_row(P, b, s);
     // TAIL: drafted ids now (consumed after the loop), their logits right after it, so a
     // workgroup that turns out to be its sequence's last arrival has them in registers
-    int64_t pf_tok = -1;
-    if (TAIL && threadIdx.x < P.gamma) pf_tok = P.draft_tokens[b * P.tok_stride + threadIdx.x];
+    DraftPf pf;
+    const int pf_i = TAIL ? pf_draft(P) : -1;
+    if (TAIL) pf_early(P, b, pf_i, pf);
     const bool is_t = s < P.n_tslots;
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
@@ -395,8 +447,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < hi) ? load_one<DT>(row, e0 + k) : 0.f;
         consume(x, e0, std::true_type{});
     }
-    float pf_xt = 0.f, pf_xd = 0.f;
-    if (TAIL && threadIdx.x < P.gamma) fetch_drafted(P, b, threadIdx.x, pf_tok, &pf_xt, &pf_xd);
+    if (TAIL) pf_late(P, b, pf_i, pf);
     // workgroup combine (fixed order): DPP wave merge, then the 4 waves through LDS
     merge_step<kDppQuad1032>(m, acc);
     merge_step<kDppQuad2301>(m, acc);
@@ -421,7 +472,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
         __syncthreads();
         SD_TS(wg_id, 2);
         if (s_last) {
-            decide_seq(P, b, pf_tok, pf_xt, pf_xd, wg_id);
+            decide_seq(P, b, pf, wg_id);
             SD_TS(wg_id, 3);
         }
     }
@@ -512,36 +563,6 @@ __device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* x
         if (P.draft_is_probs) *xd = static_cast<const float*>(P.drow[i])[b * P.dstride + tok];
         else *xd = load_dyn(P.ddt, row_ptr(P, b * P.slots + P.n_tslots + i, &dt, &T, &keep), tok);
     }
-}
-
-// p(x_i), q(x_i) from the fetched raw values and the row stats (threads < γ; after a barrier)
-__device__ void seq_ratios_from(const Plan& P, int b, const float2* lstat, const float* lxt, const float* lxd,
-                                float* lp, float* lq, const int64_t* ltok) {
-    if (threadIdx.x >= P.gamma) return;
-    const int i = threadIdx.x;
-    const int64_t tok = ltok[i];
-    float p = 0.f, q = 0.f;
-    if (tok >= 0 && tok < P.V) {
-        const int rt = b * P.slots + i;
-        const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-        const float yt = P.tdt == SD_BF16 ? process_value<SD_BF16>(lxt[i], tok, P.tT, P.t_keep, kt)
-                       : P.tdt == SD_F32 ? process_value<SD_F32>(lxt[i], tok, P.tT, P.t_keep, kt)
-                                         : process_value<SD_F16>(lxt[i], tok, P.tT, P.t_keep, kt);
-        p = round_dyn(P.tdt, sd_exp(yt - lstat[i].x) / lstat[i].y);
-        if (P.draft_is_probs) {
-            q = lxd[i];
-        } else {
-            const int rd = b * P.slots + P.n_tslots + i;
-            const RowKeep kd = P.d_keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
-            const float2 sd = lstat[P.n_tslots + i];
-            const float yd = P.ddt == SD_BF16 ? process_value<SD_BF16>(lxd[i], tok, P.dT, P.d_keep, kd)
-                           : P.ddt == SD_F32 ? process_value<SD_F32>(lxd[i], tok, P.dT, P.d_keep, kd)
-                                             : process_value<SD_F16>(lxd[i], tok, P.dT, P.d_keep, kd);
-            q = round_dyn(P.ddt, sd_exp(yd - sd.x) / sd.y);
-        }
-    }
-    lp[i] = p;
-    lq[i] = q;
 }
 
 // p(x_i), q(x_i) of the γ drafts (threads < γ; call after seq_stats + barrier)
@@ -694,34 +715,135 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
     }
 }
 
+// p(x_i), q(x_i) of draft i from its prefetch and the rows' (m, S)
+__device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const DraftPf& pf, float2 mst, float2 msd,
+                                            float& p, float& q) {
+    p = 0.f;
+    q = 0.f;
+    if (pf.tok < 0 || pf.tok >= P.V) return;
+    const int rt = b * P.slots + i;
+    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const float yt = P.tdt == SD_BF16 ? process_value<SD_BF16>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
+                   : P.tdt == SD_F32 ? process_value<SD_F32>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
+                                     : process_value<SD_F16>(pf.xt, pf.tok, P.tT, P.t_keep, kt);
+    p = round_dyn(P.tdt, sd_exp(yt - mst.x) / mst.y);
+    if (P.draft_is_probs) {
+        q = pf.xd;
+        return;
+    }
+    const int rd = b * P.slots + P.n_tslots + i;
+    const RowKeep kd = P.d_keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const float yd = P.ddt == SD_BF16 ? process_value<SD_BF16>(pf.xd, pf.tok, P.dT, P.d_keep, kd)
+                   : P.ddt == SD_F32 ? process_value<SD_F32>(pf.xd, pf.tok, P.dT, P.d_keep, kd)
+                                     : process_value<SD_F16>(pf.xd, pf.tok, P.dT, P.d_keep, kd);
+    q = round_dyn(P.ddt, sd_exp(yd - msd.x) / msd.y);
+}
+
 // Perf-mode decision of sequence b by one 256-thread workgroup (the k_stats tail): row stats
-// from the partials (published to rowstat for the sampling pass), p/q at the drafted ids, the
-// accept walk on Philox uniforms.
-__device__ void decide_seq(const Plan& P, int b, int64_t pf_tok, float pf_xt, float pf_xd, int wg_id) {
+// from the partials (published to rowstat), p/q at the drafted ids, the accept tests on Philox
+// uniforms, the walk.  Every per-draft input was prefetched during the stream (DraftPf), so the
+// tail has one memory round trip (the partials).  With the drafter stats prefetched (P.dstats)
+// the wave that reduces target slot i tests draft i at once: one barrier before the walk.
+__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
-    __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA], lxt[SD_MAX_GAMMA], lxd[SD_MAX_GAMMA];
-    __shared__ int64_t ltok[SD_MAX_GAMMA];
-    __shared__ uint8_t lstop[SD_MAX_GAMMA];
-    if (threadIdx.x < P.gamma) {   // prefetched by the caller; stop flags now, overlapping seq_stats
-        ltok[threadIdx.x] = pf_tok;
-        lxt[threadIdx.x] = pf_xt;
-        lxd[threadIdx.x] = pf_xd;
-        lstop[threadIdx.x] = is_stop(P, pf_tok);
+    __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
+    __shared__ uint8_t lacc[SD_MAX_GAMMA], lstop[SD_MAX_GAMMA];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kThreads / kWave;
+    const int i = pf_draft(P);
+    if (i >= 0) lstop[i] = pf.stop;
+    if (P.dstats && P.n_chunks <= kWave) {
+        if (i >= 0) {
+            lstat[P.n_tslots + i] = pf.ds;
+            P.rowstat[b * P.slots + P.n_tslots + i] = pf.ds;
+        }
+        constexpr int kMaxSlotsPerWave = (SD_MAX_GAMMA + 1 + 3) / 4;
+        float2 v[kMaxSlotsPerWave];
+#pragma unroll
+        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
+            const int s = w + k * nw;
+            v[k] = (s < P.n_tslots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
+                                                         : make_float2(-INFINITY, 0.f);
+        }
+#pragma unroll
+        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
+            const int s = w + k * nw;
+            if (s >= P.n_tslots) break;
+            const float m = wave_max(v[k].x);
+            const float sum = wave_sum(v[k].x > -INFINITY ? v[k].y * sd_exp(v[k].x - m) : 0.f);
+            const float2 ms = make_float2(m, sum);
+            if (lane == 0) {
+                lstat[s] = ms;
+                P.rowstat[b * P.slots + s] = ms;
+            }
+            if (lane == k && i == s) {   // i < γ: this thread holds draft s
+                float p, q;
+                draft_ratio(P, b, i, pf, ms, pf.ds, p, q);
+                lp[i] = p;
+                lq[i] = q;
+                lacc[i] = accept_draft(P, p, q, pf.u);
+            }
+        }
+        __syncthreads();
+        SD_TS(wg_id, 4);
+        SD_TS(wg_id, 5);
+    } else {
+        seq_stats(P, b, lstat, true);   // every wave reduces partials
+        __syncthreads();
+        SD_TS(wg_id, 4);
+        if (i >= 0) {
+            float p, q;
+            draft_ratio(P, b, i, pf, lstat[i], P.draft_is_probs ? make_float2(0.f, 1.f) : lstat[P.n_tslots + i], p, q);
+            lp[i] = p;
+            lq[i] = q;
+            lacc[i] = accept_draft(P, p, q, pf.u);
+        }
+        __syncthreads();
+        SD_TS(wg_id, 5);
     }
-    seq_stats(P, b, lstat, true);       // every wave reduces partials
-    __syncthreads();
-    SD_TS(wg_id, 4);
-    seq_ratios_from(P, b, lstat, lxt, lxd, lp, lq, ltok);
-    __shared__ uint8_t lacc[SD_MAX_GAMMA];
-    if (threadIdx.x < P.gamma) {   // every draft's uniform and accept test in parallel
-        bool ovr = false;
-        lacc[threadIdx.x] = accept_draft(P, lp[threadIdx.x], lq[threadIdx.x], draw_uniform(P, b, threadIdx.x, 0, &ovr));
-    }
-    __syncthreads();
-    SD_TS(wg_id, 5);
-    if (threadIdx.x == 0) {
-        int64_t used;
-        Decision d = walk_core(P, b, lp, lq, 0, &used, lacc, lstop);
+    // the walk (walk_core's rules) from two ballots over the drafts' flags
+    if (threadIdx.x < kWave) {
+        const int g = P.gamma;
+        const bool in = lane < g;
+        const bool acc = in && lacc[lane] != 0;
+        const uint64_t rejm = __ballot(in && !acc), stopm = __ballot(in && lstop[lane] != 0);
+        const int f_rej = rejm ? __builtin_ctzll(rejm) : g;             // first rejected draft (g: none)
+        const uint64_t before = f_rej >= 64 ? ~0ull : ((1ull << f_rej) - 1ull);
+        const uint64_t stop_acc = stopm & before;                        // stop tokens among the accepted
+        if (lane != 0) return;
+        Decision d{};
+        d.stop_index = -1;
+        d.noise_off = 0;
+        if (P.rule == SD_RULE_SPEC) {
+            d.n = f_rej;
+            if (stop_acc) {
+                d.stop_index = __builtin_ctzll(stop_acc);
+                d.mode = kModeNone;
+                d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
+            } else {
+                if (f_rej == g) { d.mode = kModeBonus; d.slot = g; d.status = SD_ROW_DONE | SD_ROW_BONUS; }
+                else if (P.skip_adj) { d.mode = kModePRow; d.slot = f_rej; d.status = SD_ROW_DONE | SD_ROW_FALLBACK_P; }
+                else { d.mode = kModeResid; d.slot = f_rej; d.status = SD_ROW_DONE | SD_ROW_RESIDUAL; }
+                d.noise_off = g;
+            }
+        } else {
+            d.mode = kModeNone;
+            d.n = 0;
+            if (pf.act) {
+                d.status = SD_ROW_DONE;
+                if (stop_acc) {
+                    d.n = __builtin_ctzll(stop_acc) + 1;
+                    d.status |= SD_ROW_FINISHED;
+                } else if (f_rej < g) {
+                    d.n = f_rej;
+                    d.mode = kModeResid;
+                    d.slot = f_rej;
+                    d.status |= SD_ROW_RESIDUAL;
+                    d.noise_off = f_rej + 1;
+                } else {
+                    d.n = g;
+                }
+            }
+        }
         if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision
             d.mst = lstat[d.slot];
             d.msd = d.mode == kModeResid && !P.draft_is_probs ? lstat[P.n_tslots + d.slot] : make_float2(0.f, 1.f);
@@ -734,13 +856,11 @@ __device__ void decide_seq(const Plan& P, int b, int64_t pf_tok, float pf_xt, fl
 // grid (B): decide_seq as its own launch (perf mode without the k_stats tail)
 __global__ void __launch_bounds__(kThreads) k_decide_perf(Plan P) {
     const int b = blockIdx.x;
-    float xt = 0.f, xd = 0.f;
-    int64_t tok = -1;
-    if (threadIdx.x < P.gamma) {
-        tok = P.draft_tokens[b * P.tok_stride + threadIdx.x];
-        fetch_drafted(P, b, threadIdx.x, tok, &xt, &xd);
-    }
-    decide_seq(P, b, tok, xt, xd, 8192 - 1 - b);
+    DraftPf pf;
+    const int i = pf_draft(P);
+    pf_early(P, b, i, pf);
+    pf_late(P, b, i, pf);
+    decide_seq(P, b, pf, 8192 - 1 - b);
 }
 
 // ------------------------------------------------------------------ k_resample
@@ -885,7 +1005,7 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
 
 // STREAM (parity) mode: the decision comes from the serial k_decide -> k_walk stages.
 template <int TDT, int DDT, int EPT, bool FAST>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_resample(Plan P) {
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_resample(Plan P) {
     const int b = blockIdx.y, c = blockIdx.x;
     const Decision d = P.dec[b];
     if (d.mode == kModeNone || (d.status & SD_ROW_NOISE_OVERRUN)) return;
@@ -1110,7 +1230,11 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
     for (int k = 0; k < VEC; ++k) {
         const int64_t j = e0 + k;
         const float yt = FAST ? xt[k] : process_value<TDT>(xt[k], j, R.tT, R.t_keep, R.kt);
+#ifdef SD_EXACT_SAMPLE_PROB
         const float p = prob_exact<TDT>(yt, R.mst.x, R.mst.y, R.t_inv);
+#else
+        const float p = prob_fast<TDT>(yt, R.mst.x, R.t_inv);
+#endif
         float v = p;
         if (R.resid) {
             float q;
@@ -1118,7 +1242,11 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
                 q = xd[k];
             } else {
                 const float yd = FAST ? xd[k] : process_value<DDT>(xd[k], j, R.dT, R.d_keep, R.kd);
+#ifdef SD_EXACT_SAMPLE_PROB
                 q = prob_exact<DDT>(yd, R.msd.x, R.msd.y, R.d_inv);
+#else
+                q = prob_fast<DDT>(yd, R.msd.x, R.d_inv);
+#endif
             }
             const float diff = p - q;
             v = diff > 0.f ? diff : 0.f;
@@ -1158,31 +1286,46 @@ __device__ __forceinline__ int chunk_pick(const float* wv, double u, float pextr
         s_ptot[w] = wp;
     }
     __syncthreads();
-    double T = 0.0;
+    // wave offset first, then the lane's bounds from it: lane 63's end is the next wave's offset
+    double T = 0.0, woff = 0.0;
     float PT = 0.f;
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
-        if (k < w) excl += s_wtot[k];
+        if (k == w) woff = T;
         T += s_wtot[k];
         PT += s_ptot[k];
     }
+    excl += woff;
+    const double end = woff + wincl;
     total = T;
     ptotal = PT;
     const double t = u * T;
-    // the thread whose interval [excl, excl + its weights) holds t finds the element
-    int mypos = INT_MAX, lastp = -1;
-    double run = excl;
+    // Thread intervals [excl, end) tile the running total exactly (end is the scan's own inclusive
+    // value, which is the next thread's excl), so at most one thread holds t and only it walks its
+    // elements; the wave's last thread with positive weight finds its last positive element for
+    // the rounding fallback.  Every other lane skips the per-element loop.
+    const bool hit = tot > 0.0 && excl <= t && t < end;
+    const uint64_t hm = __ballot(hit), lm = __ballot(tot > 0.0);
+    const int last_lane = lm ? 63 - __builtin_clzll(lm) : -1;
+    if (hit || lane == last_lane) {
+        int mypos = INT_MAX, lastp = -1;
+        double run = excl;
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-        run += (double)wv[k];
-        if (wv[k] > 0.f) {
-            lastp = threadIdx.x * EPT + k;
-            if (run > t && mypos == INT_MAX && excl <= t) mypos = threadIdx.x * EPT + k;
+        for (int k = 0; k < EPT; ++k) {
+            run += (double)wv[k];
+            if (wv[k] > 0.f) {
+                lastp = threadIdx.x * EPT + k;
+                if (run > t && mypos == INT_MAX) mypos = threadIdx.x * EPT + k;
+            }
         }
+        // the hit thread's own rounding fallback: its last positive element
+        if (hit) s_pos[w] = mypos != INT_MAX ? mypos : lastp;
+        if (lane == last_lane) s_lastp[w] = lastp;
     }
-    const uint64_t hm = __ballot(mypos != INT_MAX), lm = __ballot(lastp >= 0);
-    if (lane == (hm ? __builtin_ctzll(hm) : 0)) s_pos[w] = hm ? mypos : INT_MAX;
-    if (lane == (lm ? 63 - __builtin_clzll(lm) : 0)) s_lastp[w] = lm ? lastp : -1;
+    if (lane == 0) {
+        if (!hm) s_pos[w] = INT_MAX;
+        if (!lm) s_lastp[w] = -1;
+    }
     __syncthreads();
     int pos = INT_MAX, lp = -1;
 #pragma unroll
@@ -1203,12 +1346,18 @@ __device__ __forceinline__ int64_t chunk_elem(int64_t base, int pos) {
 }
 
 // The chunk of sequence b (whole workgroup; chunk totals lw staged in LDS): the first whose fp64
-// running total in chunk order exceeds U * Σ, U = Philox U[0,1) at 53 bits; -1: no positive total.
-__device__ __forceinline__ int pick_chunk(const Plan& P, int b, const float* lw) {
+// running total in chunk order exceeds u * Σ, u = cdf_uniform(noise, b) (Philox U[0,1) at 53 bits,
+// computed by the caller ahead of the tail); -1: no positive total.
+__device__ __forceinline__ int pick_chunk(const Plan& P, double u, const float* lw) {
     __shared__ int s_chunk;
     const int lane = threadIdx.x & 63;
-    if (threadIdx.x < kWave) {
-        const double u = cdf_uniform(P.noise, (uint32_t)b);
+    if (threadIdx.x < kWave && P.rn_chunks <= kWave) {   // one scan serves both passes
+        const float sv = lane < P.rn_chunks ? lw[lane] : 0.f;
+        const double incl = wave_incl_scan_d((double)sv);
+        const double t = u * lane_d(incl, 63);
+        const uint64_t hit = __ballot(incl > t && sv > 0.f), pos = __ballot(sv > 0.f);
+        if (lane == 0) s_chunk = hit ? __builtin_ctzll(hit) : (pos ? 63 - __builtin_clzll(pos) : -1);
+    } else if (threadIdx.x < kWave) {
         int chunk = -1, lastpos = -1;
         double total = 0.0;
         for (int c0 = 0; c0 < P.rn_chunks; c0 += kWave) {   // pass 1 (one group for V <= 128 Ki)
@@ -1239,14 +1388,17 @@ __device__ __forceinline__ int pick_chunk(const Plan& P, int b, const float* lw)
 // trip: engine-state read issued first, every chunk partial staged into LDS in one cooperative
 // load.  Only the engine's den <= 1e-12 fallback re-reads a chunk (its p weights).
 template <int TDT, int DDT, bool FAST, bool STOCH>
-__device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, int b, PairRows R, int wg_id) {
+__device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, int b, PairRows R, double u_row,
+                                              int wg_id) {
     constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
     int64_t acc0 = 0;
     if (threadIdx.x == 0 && engine_state && (d.status & SD_ROW_DONE)) acc0 = P.accepted_count[b];   // early
-    __shared__ int64_t lstops[kLdsStops];   // wave 0 stages the stop list (read by thread 0 at the end)
-    if (threadIdx.x < P.n_stop && threadIdx.x < kLdsStops) lstops[threadIdx.x] = P.stops[threadIdx.x];
+    // the stop list into registers now, into LDS after the partials' loads are issued (one round trip)
+    __shared__ int64_t lstops[kLdsStops];   // read by thread 0 at the end
+    const bool stop_lane = threadIdx.x < P.n_stop && threadIdx.x < kLdsStops;
+    const int64_t stop_v = stop_lane ? P.stops[threadIdx.x] : 0;
     int64_t x = -1;
     float mass = NAN;
     int32_t status = d.status;
@@ -1261,6 +1413,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
                 l_pv[k] = ld_coh(&rp[k].pval);
                 l_cand[k] = ld_coh(&rp[k].pidx);
             }
+            if (stop_lane) lstops[threadIdx.x] = stop_v;
             __syncthreads();
             if (threadIdx.x < kWave) {   // Σ residual, fixed order (lane-strided, then a butterfly)
                 float sacc = 0.f;
@@ -1273,7 +1426,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
             SD_TS(wg_id, 4);
             // engine/infer_engine.py:319-321: den <= 1e-12 -> multinomial(p) over the target row
             const bool fallback = d.mode == kModeResid && P.rule == SD_RULE_ENGINE && (double)S <= 1e-12;
-            const int c = pick_chunk(P, b, fallback ? l_pv : l_sum);
+            const int c = pick_chunk(P, u_row, fallback ? l_pv : l_sum);
             SD_TS(wg_id, 7);
             if (c >= 0 && !fallback) {
                 x = l_cand[c];
@@ -1313,7 +1466,7 @@ __device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
 // grid (chunk, B).  STOCH: chunk Σ weight; greedy (!STOCH): the exact argmax-candidate bodies.
 // TAIL: the last workgroup of each sequence runs sample_finish; otherwise k_sample_finish does.
 template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_sample(Plan P) {
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const int wg_id = 8192 + blockIdx.y * gridDim.x + blockIdx.x;
@@ -1322,6 +1475,8 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     else { b = blockIdx.y; c = blockIdx.x; }
     SD_TS(wg_id, 0);
     const Decision d = load_decision(P, b);
+    // the tail's chunk-pick uniform, computed while the decision load is in flight
+    const double u_row = STOCH && TAIL ? cdf_uniform(P.noise, (uint32_t)b) : 0.0;
     PairRows R{};
     if (d.mode != kModeNone) {
         if constexpr (STOCH) {
@@ -1364,7 +1519,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
         __syncthreads();
         SD_TS(wg_id, 3);
         if (!s_last) return;
-        sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, wg_id);
+        sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, u_row, wg_id);
     }
 }
 
@@ -1377,7 +1532,7 @@ __global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
     PairRows R{};
     if (STOCH && d.mode != kModeNone) R = pair_rows<TDT, DDT>(P, d, b);
     SD_TS(16384 - 1 - b, 1);
-    sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, 16384 - 1 - b);
+    sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, STOCH ? cdf_uniform(P.noise, (uint32_t)b) : 0.0, 16384 - 1 - b);
 }
 
 // ------------------------------------------------------------------ sd_sample kernels
@@ -1472,7 +1627,7 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
 // P(j) = e^{y_j-M} / S, the softmax of the processed row, with no second pass over it.
 // Greedy rows keep the exact two-pass argmax (rounded-probability ties need (M, S) first).
 template <int DT, bool FAST, int NST>
-__global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80))) k_draw(Plan P) {
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     constexpr int VEC = Elem<DT>::kVec, STEP = kThreads * VEC, EPT = NST * VEC;
     __shared__ float lm[kThreads / kWave];
     const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
@@ -1484,6 +1639,10 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
     const RowKeep kp = (!FAST && P.t_keep) ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const int64_t base = (int64_t)c * NST * STEP;
+    // both uniforms up front (ALU only), overlapping the loads: the span's in-chunk draw and, in
+    // case this workgroup is the row's last arrival, the tail's chunk pick
+    const double u_c = cdf_uniform(P.noise, (uint32_t)r, 1u + (uint32_t)c);
+    const double u_row = cdf_uniform(P.noise, (uint32_t)r);
     float y[EPT];
 #pragma unroll
     for (int v = 0; v < NST; ++v) {
@@ -1517,7 +1676,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     for (int k = 0; k < EPT; ++k) wv[k] = m > -INFINITY ? __builtin_amdgcn_exp2f((y[k] - m) * kLog2e) : 0.f;
     double T;
     float PT;
-    const int pos = chunk_pick<EPT>(wv, cdf_uniform(P.noise, (uint32_t)r, 1u + (uint32_t)c), nan ? 1.f : 0.f, T, PT);
+    const int pos = chunk_pick<EPT>(wv, u_c, nan ? 1.f : 0.f, T, PT);
     SD_TS(wg_id, 2);
     // the candidate's processed value, from the thread that holds it
     __shared__ float s_ycand;
@@ -1574,7 +1733,7 @@ __global__ void __launch_bounds__(kThreads) __attribute__((amdgpu_num_sgpr(80)))
     }
     __syncthreads();
     const float2 ms = s_ms;
-    const int cp = pick_chunk(P, r, l_w);
+    const int cp = pick_chunk(P, u_row, l_w);
     SD_TS(wg_id, 5);
     if (threadIdx.x == 0) {
         int32_t st = SD_ROW_DONE;
@@ -1681,15 +1840,18 @@ bool valid_proc(const sd_processor& p) {
 }
 bool needs_keep(const sd_processor& p) { return p.kind >= SD_PROC_TOPK; }
 
-// Span of a k_stats workgroup: a multiple of one 2048-element stage, sized so the whole grid is
-// resident at once (<= 2048 workgroups = 256 CUs x 8): a grid a little over one residency
-// wave would run its remainder on 1/8 of the chip.  SD_STATS_STAGES overrides (tuning).
-void set_stats_chunks(sd::Plan& P, int rows) {
+// Span of a k_stats workgroup: a multiple of one 2048-element stage, sized for about 512
+// workgroups (2 per CU), all resident at once.  Measured at the bench shape (128 rows of 128256
+// bf16): 512 workgroups 13.6 us, 1024 14.4, 2048 16.3, 384 14.7, 256 15.9 — longer spans mean
+// fewer arrivals and partials per sequence for the decision tail, until the stream itself thins
+// out.  SD_STATS_STAGES overrides (tuning).
+// Other callers (sd_sample's greedy / STREAM statistics, A11) keep target_wgs = 2048.
+void set_stats_chunks(sd::Plan& P, int rows, int target_wgs = 2048) {
     const int64_t stage = kThreads * 8;
     const int64_t stages_per_row = (P.V + stage - 1) / stage;
-    int64_t per_wg = (rows * stages_per_row + 2047) / 2048;
+    int64_t per_wg = (rows * stages_per_row + target_wgs - 1) / target_wgs;
     if (const char* e = getenv("SD_STATS_STAGES")) per_wg = atoi(e);
-    per_wg = per_wg < 1 ? 1 : (per_wg > 16 ? 16 : per_wg);
+    per_wg = per_wg < 1 ? 1 : (per_wg > 64 ? 64 : per_wg);
     P.chunk = (int32_t)(per_wg * stage);
     P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
     P.stats_interleave = 0;   // measured: contiguous spans 38.4 us/step vs interleaved 39.2
@@ -1827,6 +1989,9 @@ int32_t launch_draw_dt(const sd::Plan& P, int nst, void* stream) {
     if (nst == 1) {
         if (fast) SD_LAUNCH((k_draw<DT, true, 1>), grid, dim3(kThreads), stream, P);
         else SD_LAUNCH((k_draw<DT, false, 1>), grid, dim3(kThreads), stream, P);
+    } else if (nst == 4) {
+        if (fast) SD_LAUNCH((k_draw<DT, true, 4>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_draw<DT, false, 4>), grid, dim3(kThreads), stream, P);
     } else {
         if (fast) SD_LAUNCH((k_draw<DT, true, 2>), grid, dim3(kThreads), stream, P);
         else SD_LAUNCH((k_draw<DT, false, 2>), grid, dim3(kThreads), stream, P);
@@ -1835,11 +2000,12 @@ int32_t launch_draw_dt(const sd::Plan& P, int nst, void* stream) {
 }
 
 int32_t launch_draw(sd::Plan& P, void* stream) {
-    // spans of NST stages (2048 elements each): 1 while the grid fits one residency wave
+    // spans of NST stages (2048 elements each): 2 once the grid passes ~1024 workgroups
+    // (measured at 32 rows of 128256 bf16: NST 1 9.0 us, 2 8.5, 4 10.6 — its registers spill)
     const int64_t stage = kThreads * 8;
     const int64_t nst_row = (P.V + stage - 1) / stage;
-    int nst = P.B * nst_row <= 2048 ? 1 : 2;
-    if (const char* e = getenv("SD_DRAW_STAGES")) nst = atoi(e) == 2 ? 2 : 1;
+    int nst = P.B * nst_row <= 1024 ? 1 : 2;
+    if (const char* e = getenv("SD_DRAW_STAGES")) nst = atoi(e) == 4 ? 4 : (atoi(e) == 2 ? 2 : 1);
     if (P.tdt == SD_F32) nst = 2;   // fp32 stages hold 1024 elements: keep spans >= 2048 (workspace sizing)
     const int64_t step = kThreads * (int64_t)(P.tdt == SD_F32 ? 4 : 8);
     P.chunk = (int32_t)(nst * step);
@@ -1932,8 +2098,7 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         P.stat_slots = P.n_tslots;
     }
 
-    const int rows = P.B * P.slots;
-    set_stats_chunks(P, rows);
+    set_stats_chunks(P, P.B * P.stat_slots, 512);   // the rows k_stats streams
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->batch * (2 * a->gamma + 1), a->batch, a->gamma, a->vocab);
 
