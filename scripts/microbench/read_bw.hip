@@ -73,12 +73,14 @@ int main() {
     uint4* p; float* out;
     CK(hipMalloc(&p, big)); CK(hipMalloc(&out, 1 << 20));
     CK(hipMemset(p, 0x3f, big));
-    for (long bytes : {64l << 20, big}) {
-        for (int grid : {1024, 2048, 4096, 8192}) {
+    for (long bytes : {32l << 20, 64l << 20, big}) {
+        for (int grid : {256, 512, 1024, 2048, 4096, 8192}) {
             run<0, 4>("xor", p, bytes, grid, out);
             run<1, 4>("exp", p, bytes, grid, out);
             run<2, 4>("online", p, bytes, grid, out);
         }
+        run<0, 8>("xor", p, bytes, 512, out);
+        run<0, 8>("xor", p, bytes, 1024, out);
         run<0, 8>("xor", p, bytes, 2048, out);
         run<2, 8>("online", p, bytes, 2048, out);
         run<0, 1>("xor", p, bytes, 2048, out);
