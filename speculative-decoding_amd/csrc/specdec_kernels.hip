@@ -100,6 +100,10 @@ struct Plan {
     Decision* dec;
     ResPart* rpart;
     int32_t* keep_hist;   // threshold scratch
+    uint32_t* thr_part;   // 16-bit thresholds (sd_threshold.inc): per (row, slice) max key | NaN-inf flag
+    float* thr_tail;      //   per (row, slice) Σexp below the window / tie counts
+    int32_t* thr_hist;    //   per-row key histogram (global atomics)
+    struct ThrRow* thr;   //   per-row tie request
     uint32_t* cnt;        // per-sequence arrival counters (seq_counter): set 0 k_stats, set 1 k_sample
     uint64_t* ts;         // SD_PHASE_TIMING builds only: per-workgroup phase timestamps
     int32_t tails;        // perf mode: decide / finish in last-arrival tails (1) or own launches (0)
@@ -1830,6 +1834,10 @@ void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     P.dec = c.take<Decision>(B);
     P.rpart = c.take<ResPart>((size_t)(B > rows_total ? B : rows_total) * nc);
     P.keep_hist = c.take<int32_t>((size_t)rows_total * kThreshScratchInts);
+    P.thr_part = c.take<uint32_t>((size_t)rows_total * kThrMaxSlices);
+    P.thr_tail = c.take<float>((size_t)rows_total * kThrMaxSlices);
+    P.thr_hist = c.take<int32_t>((size_t)rows_total * kThrWin);
+    P.thr = c.take<ThrRow>(rows_total);
 }
 
 bool valid_dtype(int dt) { return dt == SD_F32 || dt == SD_BF16 || dt == SD_F16; }
@@ -2160,13 +2168,13 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);
+#ifdef SD_PHASE_TIMING
+    if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
+#endif
     if (P.t_keep) {
         const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
         if (st != SD_OK) return st;
     }
-#ifdef SD_PHASE_TIMING
-    if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
-#endif
     if (P.noise.mode == SD_NOISE_PHILOX && P.t_stoch) {
         if (P.B > kCntMax || max_chunks(P.V) > kTailChunks) return SD_ERR_UNSUPPORTED;
         return launch_draw(P, stream);   // one pass; the row's last arrival writes the outputs
