@@ -13,7 +13,8 @@ using namespace sd;
 constexpr int kV = 128256, kStep = 2048;
 
 // VAR 0: branchy online (product), 1: branch-free online (rescale every vector),
-// 2: fixed reference max (no online), 3: xor only (no math)
+// 2: fixed reference max (no online), 3: xor only (no math), 4: lazy reference m (k_stats),
+// 5: lazy reference m with packed f32 math (v_pk_fma / v_pk_add)
 template <int VAR, int PIPE>
 __global__ void __launch_bounds__(256) k_var(const uint16_t* rows, int chunk, int n_chunks, float2* part) {
     const int r = blockIdx.y, c = blockIdx.x;
@@ -25,6 +26,33 @@ __global__ void __launch_bounds__(256) k_var(const uint16_t* rows, int chunk, in
     auto consume = [&](const float* y) {
         if (VAR == 3) { for (int k = 0; k < 8; ++k) xx ^= __float_as_uint(y[k]); return; }
         if (VAR == 2) { for (int k = 0; k < 8; ++k) acc += sd_exp(y[k] - 16.f); return; }
+        if (VAR == 4 || VAR == 5) {
+            constexpr float L = 1.44269502162933349609375f;
+            float sv = 0.f;
+            if (VAR == 4) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) sv += __builtin_amdgcn_exp2f((y[k] - m) * L);
+            } else {
+                typedef float f2 __attribute__((ext_vector_type(2)));
+                const f2 mL = {-m * L, -m * L}, LL = {L, L};
+                f2 s2 = {0.f, 0.f};
+#pragma unroll
+                for (int k = 0; k < 8; k += 2) {
+                    f2 t = f2{y[k], y[k + 1]} * LL + mL;
+                    s2 += f2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)};
+                }
+                sv = s2.x + s2.y;
+            }
+            if (!(sv < 1.8446744e19f)) {
+                float vm = -INFINITY;
+                for (int k = 0; k < 8; ++k) vm = fmaxf(vm, y[k]);
+                if (vm > m) { acc = m > -INFINITY ? acc * sd_exp(m - vm) : 0.f; m = vm; }
+                sv = 0.f;
+                for (int k = 0; k < 8; ++k) sv += __builtin_amdgcn_exp2f((y[k] - m) * L);
+            }
+            acc += sv;
+            return;
+        }
         float vm = y[0];
 #pragma unroll
         for (int k = 1; k < 8; ++k) vm = fmaxf(vm, y[k]);
@@ -91,7 +119,7 @@ void run(const char* name, const uint16_t* rows, int nrows, int stages, float2* 
 }
 
 int main() {
-    const int nrows = 256;
+    const int nrows = 128;   // the bench's target rows: 32 sequences x 4
     std::vector<uint16_t> h((size_t)nrows * kV);
     std::mt19937 g(1);
     std::normal_distribution<float> nd(0.f, 3.f);
@@ -100,12 +128,13 @@ int main() {
     CK(hipMalloc(&d, h.size() * 2)); CK(hipMalloc(&part, 1 << 24));
     CK(hipMemcpy(d, h.data(), h.size() * 2, hipMemcpyHostToDevice));
     for (int st : {4, 8, 16}) {
-        run<0, 4>("branchy-online", d, nrows, st, part);
-        run<1, 4>("branchfree-online", d, nrows, st, part);
-        run<2, 4>("fixed-max", d, nrows, st, part);
         run<3, 4>("xor", d, nrows, st, part);
+        run<4, 4>("lazy", d, nrows, st, part);
+        run<5, 4>("lazy-packed", d, nrows, st, part);
+        run<4, 8>("lazy", d, nrows, st, part);
+        run<5, 8>("lazy-packed", d, nrows, st, part);
+        run<3, 8>("xor", d, nrows, st, part);
     }
-    run<0, 8>("branchy-online", d, nrows, 8, part);
-    run<0, 2>("branchy-online", d, nrows, 8, part);
+    run<2, 4>("fixed-max", d, nrows, 16, part);
     return 0;
 }
