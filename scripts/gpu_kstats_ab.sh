@@ -9,8 +9,7 @@ run() {  # $1 = tag, rest = env assignments
 }
 run base SD_NOTHING=0
 run notails SD_TAILS=0
-run noaffine SD_XCD_AFFINE=0
-run ilv0 SD_STATS_INTERLEAVE=0
-run ilv1 SD_STATS_INTERLEAVE=1
+run decsample SD_DEC_IN_SAMPLE=1
+run nounroll SD_STATS_UNROLL=0
 run st8 SD_STATS_STAGES=8
 run st32 SD_STATS_STAGES=32

@@ -107,9 +107,11 @@ struct Plan {
     uint32_t* cnt;        // per-sequence arrival counters (seq_counter): set 0 k_stats, set 1 k_sample
     uint64_t* ts;         // SD_PHASE_TIMING builds only: per-workgroup phase timestamps
     int32_t tails;        // perf mode: decide / finish in last-arrival tails (1) or own launches (0)
+    int32_t dec_in_sample;   // perf mode, stochastic rows: the decision is computed in k_sample (DEC)
     int32_t coh;          // partials may come from the same launch: read them agent-coherently
     int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
     int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
+    int32_t stats_unroll;   // k_stats: spans of <= 16 full stages fully unrolled (all loads up front)
     // sd_ngram_verify (sd_ngram.inc)
     struct NgPart* ngpart;
     int64_t* filler_ids;
@@ -297,7 +299,8 @@ __device__ __forceinline__ void pf_late(const Plan& P, int b, int i, DraftPf& pf
     bool ovr = false;
     pf.u = draw_uniform(P, b, i, 0, &ovr);   // perf mode: Philox, no stream words
 }
-__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id);
+__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out = nullptr,
+                           bool publish = true, bool coh = true);
 
 // Arrival at a per-sequence counter (thread 0, after storing its partials with st_coh): true for
 // the last of `total` arrivals, which also re-arms the counter.  coh_wait() completes the
@@ -417,7 +420,32 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     // unconditionally (the prefetch index is clamped), so the compiler keeps kPipe of them in
     // flight with counted vmcnt waits instead of draining to vmcnt(0) each stage.
     const int nfull = aligned ? cnt - (last_partial ? 1 : 0) : 0;
-    if (nfull > 0) {
+    // Spans of at most 16 full stages (the bench shape: 16) are fully unrolled with every load
+    // issued up front: no loop-carried buffer, so the compiler retires them with counted vmcnt
+    // waits in arrival order.  The rotating-buffer loop below copies its buffers between
+    // iterations, which costs an s_waitcnt vmcnt(0) every kPipe stages: the wave drains its
+    // loads and stalls a full memory latency each time (k_stats 8.6 -> see DESIGN §4).
+    // Indices past nfull are clamped (re-reads of the last stage, not consumed).
+    auto unrolled = [&](auto u) {
+        constexpr int U = decltype(u)::value;
+        const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;
+        uint4 buf[U];
+#pragma unroll
+        for (int d = 0; d < U; ++d) buf[d] = vb[stage_of(d < nfull ? d : nfull - 1) * kThreads];
+#pragma unroll
+        for (int d = 0; d < U; ++d) {
+            if (d < nfull) {
+                float x[VEC];
+                unpack16<DT>(buf[d], x);
+                consume(x, stage_of(d) * STEP + threadIdx.x * VEC, std::false_type{});
+            }
+        }
+    };
+    const bool unroll_ok = P.stats_unroll != 0;
+    if (unroll_ok && nfull > 0 && nfull <= 4) unrolled(std::integral_constant<int, 4>{});
+    else if (unroll_ok && nfull > 4 && nfull <= 8) unrolled(std::integral_constant<int, 8>{});
+    else if (unroll_ok && nfull > 8 && nfull <= 16) unrolled(std::integral_constant<int, 16>{});
+    else if (nfull > 0) {
         const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;   // stage k at vb[k * kThreads]
         uint4 buf[kPipe];
 #pragma unroll
@@ -743,12 +771,14 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
     q = round_dyn(P.ddt, sd_exp(yd - msd.x) / msd.y);
 }
 
-// Perf-mode decision of sequence b by one 256-thread workgroup (the k_stats tail): row stats
+// Perf-mode decision of sequence b by one 256-thread workgroup (the k_stats tail, or every k_sample
+// workgroup of the sequence when the decision is replicated there: out = its LDS copy, publish only
+// from one of them): row stats
 // from the partials (published to rowstat), p/q at the drafted ids, the accept tests on Philox
 // uniforms, the walk.  Every per-draft input was prefetched during the stream (DraftPf), so the
 // tail has one memory round trip (the partials).  With the drafter stats prefetched (P.dstats)
 // the wave that reduces target slot i tests draft i at once: one barrier before the walk.
-__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id) {
+__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out, bool publish, bool coh) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
     __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
     __shared__ uint8_t lacc[SD_MAX_GAMMA], lstop[SD_MAX_GAMMA];
@@ -758,14 +788,14 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id) {
     if (P.dstats && P.n_chunks <= kWave) {
         if (i >= 0) {
             lstat[P.n_tslots + i] = pf.ds;
-            P.rowstat[b * P.slots + P.n_tslots + i] = pf.ds;
+            if (publish) P.rowstat[b * P.slots + P.n_tslots + i] = pf.ds;
         }
         constexpr int kMaxSlotsPerWave = (SD_MAX_GAMMA + 1 + 3) / 4;
         float2 v[kMaxSlotsPerWave];
 #pragma unroll
         for (int k = 0; k < kMaxSlotsPerWave; ++k) {
             const int s = w + k * nw;
-            v[k] = (s < P.n_tslots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
+            v[k] = (s < P.n_tslots && lane < P.n_chunks) ? ld_x(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane, coh)
                                                          : make_float2(-INFINITY, 0.f);
         }
 #pragma unroll
@@ -777,7 +807,7 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id) {
             const float2 ms = make_float2(m, sum);
             if (lane == 0) {
                 lstat[s] = ms;
-                P.rowstat[b * P.slots + s] = ms;
+                if (publish) P.rowstat[b * P.slots + s] = ms;
             }
             if (lane == k && i == s) {   // i < γ: this thread holds draft s
                 float p, q;
@@ -791,7 +821,7 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id) {
         SD_TS(wg_id, 4);
         SD_TS(wg_id, 5);
     } else {
-        seq_stats(P, b, lstat, true);   // every wave reduces partials
+        seq_stats(P, b, lstat, publish);   // every wave reduces partials
         __syncthreads();
         SD_TS(wg_id, 4);
         if (i >= 0) {
@@ -852,8 +882,11 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id) {
             d.mst = lstat[d.slot];
             d.msd = d.mode == kModeResid && !P.draft_is_probs ? lstat[P.n_tslots + d.slot] : make_float2(0.f, 1.f);
         }
-        publish_decision(P, b, d);
-        if (P.words_used && b == 0) *P.words_used = 0;
+        if (out) *out = d;
+        if (publish) {
+            publish_decision(P, b, d);
+            if (P.words_used && b == 0) *P.words_used = 0;
+        }
     }
 }
 
@@ -1469,7 +1502,12 @@ __device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
 
 // grid (chunk, B).  STOCH: chunk Σ weight; greedy (!STOCH): the exact argmax-candidate bodies.
 // TAIL: the last workgroup of each sequence runs sample_finish; otherwise k_sample_finish does.
-template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL>
+// DEC (stochastic rows): no k_stats tail ran; every workgroup of sequence b computes the decision
+// itself from the row-statistics partials (decide_seq: one round trip for the partials and the
+// drafted ids, one for the drafted logits) and chunk 0 publishes it.  The decision then costs the
+// sampler ~1 round trip instead of a three-round-trip tail (store, counter, reload) at the end of
+// the streaming kernel.
+template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL, bool DEC = false>
 __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
@@ -1478,7 +1516,22 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     if (P.xcd_affine) affine_split(wg_id - 8192, (int)gridDim.x, b, c);
     else { b = blockIdx.y; c = blockIdx.x; }
     SD_TS(wg_id, 0);
-    const Decision d = load_decision(P, b);
+    Decision d;
+    if constexpr (DEC) {
+        __shared__ Decision s_dec;
+        DraftPf pf;
+        const int pi = pf_draft(P);
+        pf_early(P, b, pi, pf);
+        pf_late(P, b, pi, pf);
+        // partials of the previous launch: plain, cacheable loads (every workgroup of the sequence
+        // reads the same lines: coherent loads would each go to memory)
+        decide_seq(P, b, pf, wg_id, &s_dec, c == 0, false);
+        __syncthreads();
+        d = s_dec;
+        if (d.mode < kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) d.mode = kModeNone;
+    } else {
+        d = load_decision(P, b);
+    }
     // the tail's chunk-pick uniform, computed while the decision load is in flight
     const double u_row = STOCH && TAIL ? cdf_uniform(P.noise, (uint32_t)b) : 0.0;
     PairRows R{};
@@ -1864,6 +1917,8 @@ void set_stats_chunks(sd::Plan& P, int rows, int target_wgs = 2048) {
     P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
     P.stats_interleave = 0;   // measured: contiguous spans 38.4 us/step vs interleaved 39.2
     if (const char* e = getenv("SD_STATS_INTERLEAVE")) P.stats_interleave = atoi(e);
+    P.stats_unroll = 1;
+    if (const char* e = getenv("SD_STATS_UNROLL")) P.stats_unroll = atoi(e);
 }
 
 // Resample / sample passes: 1 or 2 stages of 2048 elements per workgroup, about 1024 workgroups so
@@ -1917,7 +1972,10 @@ int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
         if (fast) SD_LAUNCH((k_resample<TDT, DDT, 8, true>), grid, dim3(kThreads), stream, P);
         else SD_LAUNCH((k_resample<TDT, DDT, 8, false>), grid, dim3(kThreads), stream, P);
     } else {
-        if (P.tails) {
+        if (P.tails && P.dec_in_sample) {   // stochastic rows only (sd_verify)
+            if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true, true>), grid, dim3(kThreads), stream, P);
+            else SD_LAUNCH((k_sample<TDT, DDT, false, true, true, true>), grid, dim3(kThreads), stream, P);
+        } else if (P.tails) {
             if (P.t_stoch) {
                 if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true>), grid, dim3(kThreads), stream, P);
                 else SD_LAUNCH((k_sample<TDT, DDT, false, true, true>), grid, dim3(kThreads), stream, P);
@@ -2123,12 +2181,17 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.tails = 1;
     if (const char* e = getenv("SD_TAILS")) P.tails = atoi(e);
     P.coh = perf && P.tails;
+    // stochastic rows, opt-in (SD_DEC_IN_SAMPLE=1): the decision moves from the k_stats tail into
+    // the sampler's workgroups.  Measured slower at the bench shape (step 63.9 vs 61.9 us: k_stats
+    // loses its 5 us tail but every k_sample workgroup pays ~7 us for the decision), so off.
+    P.dec_in_sample = 0;
+    if (const char* e = getenv("SD_DEC_IN_SAMPLE")) P.dec_in_sample = perf && P.tails && P.t_stoch && atoi(e);
     P.xcd_affine = perf && P.B % 8 == 0;
     if (const char* e = getenv("SD_XCD_AFFINE")) P.xcd_affine = P.xcd_affine && atoi(e);
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
     const int reps = a->prof_stats_begin && a->prof_stats_repeat > 1 ? a->prof_stats_repeat : 1;
     for (int rep = 0; rep < reps; ++rep)
-        if (int32_t st = launch_stats(P, stream, perf && P.tails)) return st;
+        if (int32_t st = launch_stats(P, stream, perf && P.tails && !P.dec_in_sample)) return st;
     if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
     if (perf && !P.tails) SD_LAUNCH(k_decide_perf, dim3(P.B), dim3(kThreads), stream, P);
     if (!perf) {   // parity mode: the reference's serial noise order
