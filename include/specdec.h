@@ -273,6 +273,46 @@ typedef struct {
 size_t sd_ngram_workspace_size(int32_t batch, int32_t gamma, int32_t vocab);
 int32_t sd_ngram_verify(const sd_ngram_args* args, void* stream);
 
+/* Device n-gram drafter store under the reference's OneLevelNGramStorage /
+ * NGramStorage (ngram_assisted/ngram_storage.py:71-249): initialize / update / next_token /
+ * has_gram keep their meaning; the host keeps the record clock (ts) and the fallback draws.
+ *   sd_ngram_store_initialize  replaces ngram_storage.py:128-142 (one level), 227-243 (all orders)
+ *   sd_ngram_store_update      replaces ngram_storage.py:106-126, 196-217
+ *   sd_ngram_store_next_token  replaces ngram_storage.py:76-90, 162-177 (out[] holds the caller's
+ *                              torch.randint fallback draws on entry, overwritten for known grams)
+ *   sd_ngram_store_has_gram    replaces ngram_storage.py:92-102, 179-194 (writes 0/1 to *out)
+ * Records are stamped ts = ts_base + their index in the reference's processing order (initialize:
+ * b * len + i; update: b * k + j); the caller advances ts_base by batch * len / batch * k after
+ * each call.  Tables: caller-owned device memory, zero-filled once, capacities powers of two.
+ * Token ids must lie in [0, 2^17), n in [2, SD_NGRAM_MAX_N]; a full table or a bad token sets a
+ * bit in *status (the call still returns SD_OK: the condition is found on the device).          */
+#define SD_NGRAM_MAX_N 4
+#define SD_NGRAM_FULL 1
+#define SD_NGRAM_BAD_TOKEN 2
+typedef struct {
+    uint64_t* gram_keys;         /* [gram_capacity] 0 = empty                                   */
+    uint64_t* gram_best;         /* [gram_capacity] count<<44 | (2^27-1-ts)<<17 | token           */
+    int64_t gram_capacity;
+    uint64_t* pair_keys;         /* [pair_capacity] (gram slot, token)                            */
+    uint32_t* pair_count;        /* [pair_capacity]                                               */
+    uint32_t* pair_ts;           /* [pair_capacity] latest record ts                              */
+    int64_t pair_capacity;
+    int32_t* status;             /* [1] SD_NGRAM_* bits                                           */
+    int32_t n;                   /* the reference's n                                             */
+    int32_t one_level;           /* 1: OneLevelNGramStorage, 0: NGramStorage                      */
+    int32_t vocab;               /* <= 2^17                                                       */
+} sd_ngram_store;
+
+int32_t sd_ngram_store_initialize(const sd_ngram_store* store, const int64_t* ids, int32_t batch, int32_t len,
+                                  int64_t stride_b, int64_t ts_base, void* stream);
+int32_t sd_ngram_store_update(const sd_ngram_store* store, const int64_t* ids, int32_t batch, int32_t len,
+                              int64_t stride_b, const int64_t* next_tokens, int32_t k, int64_t next_stride_b,
+                              int64_t ts_base, void* stream);
+int32_t sd_ngram_store_next_token(const sd_ngram_store* store, const int64_t* ids, int32_t batch, int32_t len,
+                                  int64_t stride_b, int64_t* out, uint8_t* known, void* stream);
+int32_t sd_ngram_store_has_gram(const sd_ngram_store* store, const int64_t* ngram, int32_t len, uint8_t* out,
+                                void* stream);
+
 /* Host side: torch CPU generator state (torch.Generator.get_state(), 5056 bytes) <-> words. */
 int32_t sd_mt19937_fill(const uint8_t* torch_state, size_t state_len, uint32_t* out, int64_t n);
 int32_t sd_mt19937_advance(uint8_t* torch_state, size_t state_len, int64_t n);

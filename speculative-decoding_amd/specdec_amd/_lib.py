@@ -33,7 +33,21 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.g
 
 EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify_workspace_size", "sd_verify",
            "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",
-           "sd_ngram_workspace_size", "sd_ngram_verify", "sd_mt19937_fill", "sd_mt19937_advance")
+           "sd_ngram_workspace_size", "sd_ngram_verify", "sd_mt19937_fill", "sd_mt19937_advance",
+           "sd_ngram_store_initialize", "sd_ngram_store_update", "sd_ngram_store_next_token",
+           "sd_ngram_store_has_gram")
+
+
+SD_NGRAM_MAX_N = 4
+SD_NGRAM_FULL = 1
+SD_NGRAM_BAD_TOKEN = 2
+
+
+class sd_ngram_store(C.Structure):
+    _fields_ = [("gram_keys", C.c_void_p), ("gram_best", C.c_void_p), ("gram_capacity", C.c_int64),
+                ("pair_keys", C.c_void_p), ("pair_count", C.c_void_p), ("pair_ts", C.c_void_p),
+                ("pair_capacity", C.c_int64), ("status", C.c_void_p), ("n", C.c_int32), ("one_level", C.c_int32),
+                ("vocab", C.c_int32)]
 
 
 class sd_processor(C.Structure):
@@ -148,6 +162,15 @@ def _load():
     lib.sd_mt19937_fill.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64]
     lib.sd_mt19937_advance.restype = C.c_int32
     lib.sd_mt19937_advance.argtypes = [C.c_void_p, C.c_size_t, C.c_int64]
+    P = C.POINTER(sd_ngram_store)
+    for name, args in (("sd_ngram_store_initialize", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_void_p]),
+                       ("sd_ngram_store_update", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_int32,
+                                                  C.c_int64, C.c_int64, C.c_void_p]),
+                       ("sd_ngram_store_next_token", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p,
+                                                      C.c_void_p, C.c_void_p]),
+                       ("sd_ngram_store_has_gram", [P, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p])):
+        getattr(lib, name).restype = C.c_int32
+        getattr(lib, name).argtypes = args
     if lib.sd_abi_version() != SD_ABI_VERSION:
         raise ImportError(f"specdec_amd: ABI mismatch ({lib.sd_abi_version()} != {SD_ABI_VERSION})")
     return lib

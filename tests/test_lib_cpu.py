@@ -40,6 +40,9 @@ int main(void) {
   printf("sd_probs_args %zu\n", sizeof(sd_probs_args));
   printf("sd_noise %zu\n", sizeof(sd_noise));
   printf("sd_ngram_args %zu\n", sizeof(sd_ngram_args));
+  printf("sd_ngram_store %zu\n", sizeof(sd_ngram_store));
+  F(sd_ngram_store, gram_capacity) F(sd_ngram_store, pair_keys) F(sd_ngram_store, pair_capacity)
+  F(sd_ngram_store, status) F(sd_ngram_store, one_level) F(sd_ngram_store, vocab)
   F(sd_verify_args, draft_rows) F(sd_verify_args, draft_tokens) F(sd_verify_args, target_proc)
   F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
   F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end) F(sd_verify_args, prof_stats_repeat)
@@ -63,7 +66,7 @@ def test_ctypes_layout_matches_c_header():
     got = dict(line.rsplit(" ", 1) for line in out if line)
     for name, cls in [("sd_verify_args", _lib.sd_verify_args), ("sd_sample_args", _lib.sd_sample_args),
                       ("sd_probs_args", _lib.sd_probs_args), ("sd_noise", _lib.sd_noise),
-                      ("sd_ngram_args", _lib.sd_ngram_args)]:
+                      ("sd_ngram_args", _lib.sd_ngram_args), ("sd_ngram_store", _lib.sd_ngram_store)]:
         assert int(got[name]) == C.sizeof(cls), name
     for key, val in got.items():
         if "." in key:

@@ -55,3 +55,31 @@ def test_reset_forgets():
     s.initialize(torch.tensor([[4, 5, 6]]))
     tok, known = s.next_token(torch.tensor([[4, 5]]))
     assert known[0] and int(tok[0]) == 6
+
+
+def _best_by_stamps(records):
+    """The device store's rule (csrc/ngram_store.hip): best = argmax over tokens of (count, -latest
+    ts), with ts the record's position in the reference's processing order."""
+    cnt, last = {}, {}
+    for ts, (gram, tok) in enumerate(records):
+        cnt[(gram, tok)] = cnt.get((gram, tok), 0) + 1
+        last[(gram, tok)] = ts
+    best = {}
+    for (gram, tok), c in cnt.items():
+        key = (c, -last[(gram, tok)])
+        if gram not in best or key > best[gram][0]:
+            best[gram] = (key, tok)
+    return {gram: tok for gram, (key, tok) in best.items()}
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_order_free_best_rule_equals_the_reference_rule(seed):
+    """Pins the device store's algorithm on the CPU: for random record streams (few grams, few
+    tokens: many ties), argmax (count, -latest ts) equals the reference's incremental rule."""
+    g = torch.Generator().manual_seed(seed)
+    recs = [((int(a),), int(t)) for a, t in zip(torch.randint(0, 4, (400,), generator=g),
+                                                 torch.randint(0, 5, (400,), generator=g))]
+    store = ref.NgramStore("one", 2, 10, ref.TorchNoise(None))
+    for gram, tok in recs:
+        store._add(1, gram, [tok])
+    assert _best_by_stamps(recs) == store.best[1]
