@@ -281,6 +281,10 @@ int32_t sd_ngram_verify(const sd_ngram_args* args, void* stream);
  *   sd_ngram_store_next_token  replaces ngram_storage.py:76-90, 162-177 (out[] holds the caller's
  *                              torch.randint fallback draws on entry, overwritten for known grams)
  *   sd_ngram_store_has_gram    replaces ngram_storage.py:92-102, 179-194 (writes 0/1 to *out)
+ *   sd_ngram_store_draft       replaces the loop's gamma chained next_token calls
+ *                              (ngram_assisted/ngram_assisted.py:94-101): drafts[b, k] and known[b, k]
+ *                              (known: [B, gamma] contiguous) for the history extended by drafts
+ *                              0..k-1; fallback[b, k] = the k-th call's torch.randint draw
  * Records are stamped ts = ts_base + their index in the reference's processing order (initialize:
  * b * len + i; update: b * k + j); the caller advances ts_base by batch * len / batch * k after
  * each call.  Tables: caller-owned device memory, zero-filled once, capacities powers of two.
@@ -310,6 +314,9 @@ int32_t sd_ngram_store_update(const sd_ngram_store* store, const int64_t* ids, i
                               int64_t ts_base, void* stream);
 int32_t sd_ngram_store_next_token(const sd_ngram_store* store, const int64_t* ids, int32_t batch, int32_t len,
                                   int64_t stride_b, int64_t* out, uint8_t* known, void* stream);
+int32_t sd_ngram_store_draft(const sd_ngram_store* store, const int64_t* ids, int32_t batch, int32_t len,
+                             int64_t stride_b, int32_t gamma, const int64_t* fallback, int64_t fallback_stride_b,
+                             int64_t* drafts, int64_t drafts_stride_b, uint8_t* known, void* stream);
 int32_t sd_ngram_store_has_gram(const sd_ngram_store* store, const int64_t* ngram, int32_t len, uint8_t* out,
                                 void* stream);
 

@@ -59,4 +59,26 @@ for name, obj in (("device", DeviceNGramStorage(3, V, device="cuda")), ("host", 
         int(tok[0])   # the loop reads the draft on the host
     torch.cuda.synchronize()
     res[f"loop_step_{name}_us"] = (time.perf_counter() - t0) / 200 * 1e6
+# the n-gram loop's drafting step (configs[4]: gamma = 8): one update, then gamma chained lookups
+# read back on the host -- the host store calls next_token 8 times, the device store drafts the
+# chain in one launch (draft_chain)
+G = 8
+for name, obj in (("device", DeviceNGramStorage(3, V, device="cuda")), ("host", NGramStorage(3, V))):
+    obj.initialize(hist)
+    seq = hist
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(200):
+        x = torch.tensor([[i % 2000]])
+        obj.update(seq, x)
+        seq = torch.cat([seq, x], 1)
+        if name == "device":
+            toks = obj.draft_chain(seq, G)[0][0].tolist()
+        else:
+            s = seq[0].tolist()
+            for k in range(G):
+                tok, known = obj.next_token(torch.tensor([s]))
+                s.append(int(tok[0]))
+    torch.cuda.synchronize()
+    res[f"draft_step_g{G}_{name}_us"] = (time.perf_counter() - t0) / 200 * 1e6
 print(json.dumps(res, indent=1))

@@ -178,6 +178,47 @@ __global__ void __launch_bounds__(kThreads) k_ng_next(sd_ngram_store S, const in
     known[b] = kn;
 }
 
+// The n-gram loop's drafting (ngram_assisted/ngram_assisted.py:94-101): gamma chained next_token
+// calls, each on the history extended by the previous drafts, in one thread per history: the
+// last n-1 ids ride in registers.  fallback[b, k] = the k-th call's torch.randint draw.  Every
+// draft is produced (the caller truncates at the first unknown for stop_if_unknown).
+__global__ void __launch_bounds__(kThreads) k_ng_draft(sd_ngram_store S, const int64_t* ids, int32_t batch, int64_t len,
+                                                       int64_t stride, int32_t gamma, const int64_t* fallback,
+                                                       int64_t fstride, int64_t* drafts, int64_t dstride,
+                                                       uint8_t* known) {
+    const int b = blockIdx.x * kThreads + threadIdx.x;
+    if (b >= batch) return;
+    const int64_t* seq = ids + (int64_t)b * stride;
+    int64_t ctx[SD_NGRAM_MAX_N - 1];   // ctx[SD_NGRAM_MAX_N - 2] = newest id
+    constexpr int C = SD_NGRAM_MAX_N - 1;
+#pragma unroll
+    for (int t = 0; t < C; ++t) ctx[t] = len - C + t >= 0 ? seq[len - C + t] : -1;
+    for (int k = 0; k < gamma; ++k) {
+        const int64_t L = len + k;
+        int hi, lo;
+        if (S.one_level) hi = lo = L >= S.n - 1 ? S.n - 1 : 0;
+        else { hi = (int)(L < S.n - 1 ? L : S.n - 1); lo = 2; }
+        int64_t tok = fallback[(int64_t)b * fstride + k];
+        uint8_t kn = 0;
+        for (int j = hi; j >= lo && j >= 1; --j) {
+            uint64_t gk;
+            if (!gram_key(ctx, C, j, j, gk)) break;
+            const int64_t gs = probe<false>(S.gram_keys, S.gram_capacity, gk, S.status);
+            if (gs < 0) continue;
+            const uint64_t best = S.gram_best[gs];
+            if (best == 0) continue;
+            tok = (int64_t)(best & kTokMask);
+            kn = 1;
+            break;
+        }
+        drafts[(int64_t)b * dstride + k] = tok;
+        known[(int64_t)b * gamma + k] = kn;
+#pragma unroll
+        for (int t = 0; t + 1 < C; ++t) ctx[t] = ctx[t + 1];
+        ctx[C - 1] = tok;
+    }
+}
+
 // has_gram (ngram_storage.py:92-102, 179-194): the gram is the LAST j ids of the n-gram, its last
 // token included, as in the reference; true if that token was recorded after it
 __global__ void k_ng_has(sd_ngram_store S, const int64_t* ngram, int64_t len, uint8_t* out) {
@@ -256,6 +297,18 @@ int32_t sd_ngram_store_next_token(const sd_ngram_store* s, const int64_t* ids, i
     if (batch == 0) return SD_OK;
     hipLaunchKernelGGL(k_ng_next, dim3(blocks(batch)), dim3(kThreads), 0, (hipStream_t)stream, *s, ids, batch,
                        (int64_t)len, stride_b, out, known);
+    return launched();
+}
+
+int32_t sd_ngram_store_draft(const sd_ngram_store* s, const int64_t* ids, int32_t batch, int32_t len, int64_t stride_b,
+                             int32_t gamma, const int64_t* fallback, int64_t fallback_stride_b, int64_t* drafts,
+                             int64_t drafts_stride_b, uint8_t* known, void* stream) {
+    if (!valid_store(s) || batch < 0 || len < 0 || gamma < 0 ||
+        (batch && gamma && (!fallback || !drafts || !known || (len && !ids))))
+        return SD_ERR_INVALID;
+    if (batch == 0 || gamma == 0) return SD_OK;
+    hipLaunchKernelGGL(k_ng_draft, dim3(blocks(batch)), dim3(kThreads), 0, (hipStream_t)stream, *s, ids, batch,
+                       (int64_t)len, stride_b, gamma, fallback, fallback_stride_b, drafts, drafts_stride_b, known);
     return launched();
 }
 

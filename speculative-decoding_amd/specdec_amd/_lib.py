@@ -35,7 +35,7 @@ EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify
            "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",
            "sd_ngram_workspace_size", "sd_ngram_verify", "sd_mt19937_fill", "sd_mt19937_advance",
            "sd_ngram_store_initialize", "sd_ngram_store_update", "sd_ngram_store_next_token",
-           "sd_ngram_store_has_gram")
+           "sd_ngram_store_has_gram", "sd_ngram_store_draft")
 
 
 SD_NGRAM_MAX_N = 4
@@ -168,7 +168,9 @@ def _load():
                                                   C.c_int64, C.c_int64, C.c_void_p]),
                        ("sd_ngram_store_next_token", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p,
                                                       C.c_void_p, C.c_void_p]),
-                       ("sd_ngram_store_has_gram", [P, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p])):
+                       ("sd_ngram_store_has_gram", [P, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]),
+                       ("sd_ngram_store_draft", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int32, C.c_void_p,
+                                                 C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p])):
         getattr(lib, name).restype = C.c_int32
         getattr(lib, name).argtypes = args
     if lib.sd_abi_version() != SD_ABI_VERSION:

@@ -109,6 +109,33 @@ class _DeviceStore(INgramStorage):
                    "sd_ngram_store_next_token")
         return out, known
 
+    def draft_chain(self, input_ids: torch.Tensor, gamma: int,
+                    stop_if_unknown: bool = False) -> Tuple[torch.Tensor, torch.Tensor]:
+        """The n-gram loop's drafting (ngram_assisted/ngram_assisted.py:94-101) in one launch:
+        gamma chained ``next_token`` calls, call k on the history extended by drafts 0..k-1.
+        Returns (drafts [B, gamma], known [B, gamma]) on the device.  The fallback draws are the
+        calls' ``torch.randint(V, (B,))`` draws, taken together ((gamma, B) in one call is the
+        same stream).  With ``stop_if_unknown`` the reference stops calling after the first
+        unknown draft, so the generator is rewound and advanced by exactly the calls made (one
+        read-back, which the loop needs anyway for the drafted ids)."""
+        ids = self._ids(input_ids)
+        B, L = ids.shape
+        for k in range(gamma):
+            self._check_orders(L + k)
+        state = torch.get_rng_state() if stop_if_unknown else None
+        fb = torch.randint(self.vocab_size, size=(gamma, B)).t().contiguous().to(self.device)
+        drafts = torch.empty(B, gamma, dtype=torch.long, device=self.device)
+        known = torch.zeros(B, gamma, dtype=torch.bool, device=self.device)
+        _lib.check(_lib.lib.sd_ngram_store_draft(C.byref(self._s), ids.data_ptr(), B, L, ids.stride(0), gamma,
+                                                 fb.data_ptr(), fb.stride(0), drafts.data_ptr(), drafts.stride(0),
+                                                 known.data_ptr(), _stream(self.device)), "sd_ngram_store_draft")
+        if stop_if_unknown and gamma:
+            kn = known.all(0).cpu()   # batch 1 in the reference's loop
+            calls = gamma if bool(kn.all()) else int((~kn).nonzero()[0]) + 1
+            torch.set_rng_state(state)
+            torch.randint(self.vocab_size, size=(calls, B))
+        return drafts, known
+
     def has_gram(self, ngram: torch.Tensor) -> bool:
         g = self._ids(ngram)[0]
         res = torch.zeros(1, dtype=torch.uint8, device=self.device)

@@ -77,10 +77,17 @@ def ngram_assisted_speculative_generate(
     while cur < total_len:                                        # :95
         g = min(gamma, total_len - cur - 1)
         drafted = list(ids)
+        if hasattr(ngramstorage, "draft_chain"):                  # device store: one launch, one read-back
+            toks, knowns = ngramstorage.draft_chain(as_2d(drafted[:cur]), g, stop_if_unknown)
+            toks, knowns = toks[0].tolist(), knowns[0].tolist()
         for k in range(g):                                        # :101-105
-            tok, known = ngramstorage.next_token(as_2d(drafted[:cur + k]))
-            drafted[cur + k] = int(tok[0])
-            if not bool(known[0]) and stop_if_unknown:
+            if hasattr(ngramstorage, "draft_chain"):
+                tok_k, known_k = toks[k], knowns[k]
+            else:
+                tok, known = ngramstorage.next_token(as_2d(drafted[:cur + k]))
+                tok_k, known_k = int(tok[0]), bool(known[0])
+            drafted[cur + k] = tok_k
+            if not known_k and stop_if_unknown:
                 g = k
                 break
         speculated += g

@@ -535,9 +535,15 @@ with open(os.path.join(os.path.dirname(__file__), "golden", "ngram_loops.json"))
     NGRAM_GOLDEN = json.load(f)
 
 
+@pytest.mark.parametrize("store_kind", ["host", "device"])
 @pytest.mark.parametrize("case", sorted(NGRAM_GOLDEN))
-def test_ngram_loop_matches_reference(sd, case):
-    from specdec_amd.ngram_assisted import NGramStorage, OneLevelNGramStorage, ngram_assisted_speculative_generate
+def test_ngram_loop_matches_reference(sd, case, store_kind):
+    """The drop-in loop against the reference's own outputs, with the host drafter and with the
+    device store (sd_ngram_store_*: draft_chain drafts the gamma tokens of a step in one launch)."""
+    from specdec_amd.ngram_assisted import (DeviceNGramStorage, DeviceOneLevelNGramStorage, NGramStorage,
+                                            OneLevelNGramStorage, ngram_assisted_speculative_generate)
+    if store_kind == "device":
+        NGramStorage, OneLevelNGramStorage = DeviceNGramStorage, DeviceOneLevelNGramStorage   # noqa: N806
     from specdec_amd.utils.logits_processor import (GreedyProcessor, MultinomialProcessor, NucleusProcessor,
                                                     TopKProcessor)
     c = NGRAM_GOLDEN[case]
