@@ -182,6 +182,21 @@ __device__ __forceinline__ float2 ld_coh(const float2* p) {
 template <typename T>
 __device__ __forceinline__ T ld_x(const T* p, bool coh) { return coh ? ld_coh(p) : *p; }
 
+// One 16-byte record per write-through store / coherent load (global_*_dwordx4 sc1): a scalar
+// sc1 store is one fabric write each (dword ~6x the dwordx4 time per byte, MI355X_MICROARCH.md),
+// so a tail's partial {a, b, c, d} travels as one.  p must be 16-byte aligned.  The load waits for
+// itself (vmcnt(0)): the compiler does not track inline-asm loads.
+typedef uint32_t sd_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_coh16(void* p, uint4 v) {
+    const sd_u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" : : "v"(p), "v"(w) : "memory");
+}
+__device__ __forceinline__ uint4 ld_coh16(const void* p) {
+    sd_u32x4 w;
+    asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(w) : "v"(p) : "memory");
+    return make_uint4(w.x, w.y, w.z, w.w);
+}
+
 // this wave's coherent stores have completed (s_waitcnt 0), and the compiler keeps order
 __device__ __forceinline__ void coh_wait() {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);

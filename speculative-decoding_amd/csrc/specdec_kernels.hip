@@ -1444,11 +1444,12 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
         __shared__ int32_t l_cand[kTailChunks];
         __shared__ float s_mass;
         if (d.mode != kModeNone) {
-            const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
+            const float4* rp = reinterpret_cast<const float4*>(P.rpart) + (int64_t)b * P.rn_chunks;
             for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
-                l_sum[k] = ld_coh(&rp[k].sum);
-                l_pv[k] = ld_coh(&rp[k].pval);
-                l_cand[k] = ld_coh(&rp[k].pidx);
+                const uint4 v = ld_coh16(rp + k);
+                l_sum[k] = __uint_as_float(v.x);
+                l_pv[k] = __uint_as_float(v.y);
+                l_cand[k] = (int32_t)v.z;
             }
             if (stop_lane) lstops[threadIdx.x] = stop_v;
             __syncthreads();
@@ -1555,12 +1556,10 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
             double T;
             float PT;
             const int pos = chunk_pick<EPT>(wv, u, psum, T, PT);
-            if (threadIdx.x == 0) {
-                ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
-                st_coh(&o.sum, (float)T);
-                st_coh(&o.pval, PT);
-                st_coh(&o.pidx, pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos));
-            }
+            if (threadIdx.x == 0)   // {Σ w, Σ p, candidate}: one 16-byte record per chunk (k_draw's layout)
+                st_coh16(reinterpret_cast<float4*>(P.rpart) + (int64_t)b * P.rn_chunks + c,
+                         make_uint4(__float_as_uint((float)T), __float_as_uint(PT),
+                                    (uint32_t)(pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos)), 0u));
         } else {
             const float2 mst = P.rowstat[b * P.slots + d.slot];
             const float2 msd = d.mode == kModeResid && !P.draft_is_probs ? P.rowstat[b * P.slots + P.n_tslots + d.slot]
@@ -1745,13 +1744,13 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
         s_ycand = yc;
     }
     __syncthreads();
-    // partial (m_c, S_c | j_c, y_{j_c}) as two 8-byte coherent stores into the span's 16-byte slot
+    // partial (m_c, S_c | j_c, y_{j_c}) as one 16-byte write-through store into the span's slot
     float2* slot = reinterpret_cast<float2*>(reinterpret_cast<float4*>(P.rpart) + (int64_t)r * P.n_chunks + c);
     if (threadIdx.x == 0) {
         const float S = PT > 0.f ? NAN : (float)T;   // PT counts NaN lanes
-        st_coh(slot, make_float2(PT > 0.f && !(m > -INFINITY) ? 0.f : m, S));
-        st_coh(slot + 1, make_float2(__int_as_float(pos < 0 ? -1 : (int32_t)chunk_elem<DT, DT, EPT>(base, pos)),
-                                     pos < 0 ? -INFINITY : s_ycand));
+        st_coh16(slot, make_uint4(__float_as_uint(PT > 0.f && !(m > -INFINITY) ? 0.f : m), __float_as_uint(S),
+                                  (uint32_t)(pos < 0 ? -1 : (int32_t)chunk_elem<DT, DT, EPT>(base, pos)),
+                                  __float_as_uint(pos < 0 ? -INFINITY : s_ycand)));
     }
     __shared__ int s_last;
     if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, r), (uint32_t)P.n_chunks);
@@ -1766,7 +1765,9 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     {   // every span's partial in one staged round trip
         const float2* pr = reinterpret_cast<const float2*>(reinterpret_cast<const float4*>(P.rpart) + (int64_t)r * P.n_chunks);
         for (int k = threadIdx.x; k < P.n_chunks; k += kThreads) {
-            const float2 ms = ld_coh(pr + 2 * k), jy = ld_coh(pr + 2 * k + 1);
+            const uint4 v = ld_coh16(pr + 2 * k);
+            const float2 ms = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+            const float2 jy = make_float2(__uint_as_float(v.z), __uint_as_float(v.w));
             l_w[k] = ms.x;   // m_c for now; weights below
             l_s[k] = ms.y;
             l_cand[k] = __float_as_int(jy.x);
