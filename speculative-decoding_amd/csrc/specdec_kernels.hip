@@ -111,7 +111,6 @@ struct Plan {
     int32_t coh;          // partials may come from the same launch: read them agent-coherently
     int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
     int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
-    int32_t stats_unroll;   // k_stats: spans of <= 16 full stages fully unrolled (all loads up front)
     // sd_ngram_verify (sd_ngram.inc)
     struct NgPart* ngpart;
     int64_t* filler_ids;
@@ -420,32 +419,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     // unconditionally (the prefetch index is clamped), so the compiler keeps kPipe of them in
     // flight with counted vmcnt waits instead of draining to vmcnt(0) each stage.
     const int nfull = aligned ? cnt - (last_partial ? 1 : 0) : 0;
-    // Spans of at most 16 full stages (the bench shape: 16) are fully unrolled with every load
-    // issued up front: no loop-carried buffer, so the compiler retires them with counted vmcnt
-    // waits in arrival order.  The rotating-buffer loop below copies its buffers between
-    // iterations, which costs an s_waitcnt vmcnt(0) every kPipe stages: the wave drains its
-    // loads and stalls a full memory latency each time (k_stats 8.6 -> see DESIGN §4).
-    // Indices past nfull are clamped (re-reads of the last stage, not consumed).
-    auto unrolled = [&](auto u) {
-        constexpr int U = decltype(u)::value;
-        const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;
-        uint4 buf[U];
-#pragma unroll
-        for (int d = 0; d < U; ++d) buf[d] = vb[stage_of(d < nfull ? d : nfull - 1) * kThreads];
-#pragma unroll
-        for (int d = 0; d < U; ++d) {
-            if (d < nfull) {
-                float x[VEC];
-                unpack16<DT>(buf[d], x);
-                consume(x, stage_of(d) * STEP + threadIdx.x * VEC, std::false_type{});
-            }
-        }
-    };
-    const bool unroll_ok = P.stats_unroll != 0;
-    if (unroll_ok && nfull > 0 && nfull <= 4) unrolled(std::integral_constant<int, 4>{});
-    else if (unroll_ok && nfull > 4 && nfull <= 8) unrolled(std::integral_constant<int, 8>{});
-    else if (unroll_ok && nfull > 8 && nfull <= 16) unrolled(std::integral_constant<int, 16>{});
-    else if (nfull > 0) {
+    if (nfull > 0) {
         const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;   // stage k at vb[k * kThreads]
         uint4 buf[kPipe];
 #pragma unroll
@@ -1918,8 +1892,6 @@ void set_stats_chunks(sd::Plan& P, int rows, int target_wgs = 2048) {
     P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
     P.stats_interleave = 0;   // measured: contiguous spans 38.4 us/step vs interleaved 39.2
     if (const char* e = getenv("SD_STATS_INTERLEAVE")) P.stats_interleave = atoi(e);
-    P.stats_unroll = 1;
-    if (const char* e = getenv("SD_STATS_UNROLL")) P.stats_unroll = atoi(e);
 }
 
 // Resample / sample passes: 1 or 2 stages of 2048 elements per workgroup, about 1024 workgroups so
