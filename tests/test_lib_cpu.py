@@ -117,3 +117,22 @@ def test_mt19937_advance_large():
         r = torch.Generator().manual_seed(99)
         torch.rand(k, generator=r)
         assert torch.equal(g.get_state(), r.get_state())
+
+
+def test_no_kernel_uses_scratch():
+    """Every gfx950 kernel of libspecdec.so runs without private (scratch) memory: a kernel that
+    spills pays ~20 us per dispatch on MI355X (an unrolled k_stats variant once
+    gave the processor kernels 816 B of scratch and configs[1] nucleus +36 us per step)."""
+    llvm = "/opt/rocm/lib/llvm/bin"
+    from specdec_amd import _lib
+    if not (os.path.exists(os.path.join(llvm, "clang-offload-bundler")) and os.path.exists(os.path.join(llvm, "llvm-readelf"))):
+        pytest.skip("ROCm llvm tools not found")
+    with tempfile.TemporaryDirectory() as d:
+        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
+        subprocess.check_call(["objcopy", "--dump-section", f".hip_fatbin={fb}", _lib.LIB_PATH, os.path.join(d, "x.so")])
+        subprocess.check_call([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", f"--input={fb}", f"--output={co}",
+                               "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"])
+        notes = subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", co]).decode()
+    sizes = re.findall(r"\.private_segment_fixed_size:\s*(\d+)", notes)
+    assert len(sizes) > 100
+    assert all(int(v) == 0 for v in sizes), sorted(set(sizes))
