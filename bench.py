@@ -13,10 +13,14 @@ no collective on the data path), so scaling is weak: every rank verifies its own
 
 value = output tokens (accepted drafts + resampled tokens, all ranks) / max-over-ranks wall
 time of the K timed steps.  Steps run as hipGraph replays (the step is captured once per
-`--graph-steps` steps), noise is in-kernel Philox (perf mode).  Also reported: acceptance
-rate, the HBM roofline of the row-statistics kernel (HIP events around it, algorithmic bytes
-= every logit row read once), and the CPU baseline = the oracle (reference semantics,
-torch-CPU) timed on a bounded sample of the same workload on this host.
+`--graph-steps` steps), noise is in-kernel Philox (perf mode).  Also reported in the same line:
+acceptance rate (engine/metrics.py:123-129), per-kernel timings with the HBM roofline of the
+step's DOMINANT kernel (the largest per-step share; HIP events on the launch stream,
+algorithmic bytes = every logit row the kernel must read, once), the same step in STREAM mode
+(the reference's torch-generator noise, bit-exact tokens), the strong-scaling variant of
+configs[2] (a global batch of --batch rows split over the ranks) when N > 1, the configs[1]
+batch-1 step latencies, and the CPU baseline = the oracle (reference semantics, torch-CPU)
+timed on a bounded sample of the same workload on this host.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -25,8 +29,9 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import os
+import statistics
+import subprocess
 import sys
 import time
 
@@ -51,13 +56,118 @@ def parse():
     ap.add_argument("--sigma", type=float, default=1.0, help="drafter = target + N(0, sigma^2)")
     ap.add_argument("--graph-steps", type=int, default=20)
     ap.add_argument("--prof-steps", type=int, default=50)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stream-steps", type=int, default=5, help="STREAM-mode (bit-exact noise) steps; 0 = skip")
+    ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] batch-1 lines")
     return ap.parse_args()
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
+
+
+def graph_steps(step, steps, per_graph):
+    """Capture `per_graph` steps in one hipGraph, replay steps // per_graph times (untimed warm replay
+    first).  Returns (graph, outputs of the captured steps, replays)."""
+    G = max(1, min(per_graph, steps))
+    while steps % G:
+        G -= 1
+    graph = torch.cuda.CUDAGraph()
+    outs = []
+    with torch.cuda.graph(graph):
+        for _ in range(G):
+            outs.append(step())
+    graph.replay()
+    torch.cuda.synchronize()
+    return graph, outs, steps // G
+
+
+def timed_replays(graph, replays, dist):
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(replays):
+        graph.replay()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def engine_logits(B, g, V, sigma, seed, dev):
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    tl = (torch.randn(B, g, V, generator=gen, device=dev) * 3.0).to(torch.bfloat16)
+    dl = (tl.float() + sigma * torch.randn(B, g, V, generator=gen, device=dev)).to(torch.bfloat16)
+    return tl, dl
+
+
+class EngineStep:
+    """One engine step's sampling path over resident logits: γ drafter draws (sd_sample, one launch
+    each, engine/infer_engine.py:241-247) + one sd_verify (rule A10, :276-336)."""
+
+    def __init__(self, tl, dl, noise, row0, ops, _lib):
+        self.ops, self.lib = ops, _lib
+        B, g, V = tl.shape
+        dev = tl.device
+        self.B, self.g, self.V = B, g, V
+        self.noise, self.row0 = noise, row0
+        self.draft = torch.empty(B, g, dtype=torch.long, device=dev)
+        self.stash = type(noise).__name__ == "PhiloxNoise"
+        self.dstats = torch.empty(g, B, 2, dtype=torch.float32, device=dev)   # drafter rows' (max, Σexp)
+        self.stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
+        self.trows = [tl[:, t, :] for t in range(g)]
+        self.drows = [dl[:, t, :] for t in range(g)]
+
+    def draw(self, d):
+        self.ops.sample_rows(self.drows[d], self.ops.PLAIN_SOFTMAX, self.noise, tokens_out=self.draft[:, d],
+                             row_base=self.row0, row_stats_out=self.dstats[d] if self.stash else None)
+
+    def draws(self):
+        for d in range(self.g):
+            self.draw(d)
+
+    def verify(self, prof=None):
+        ops = self.ops
+        return ops.verify(self.trows, self.drows, self.draft, self.lib.SD_RULE_ENGINE, ops.PLAIN_SOFTMAX,
+                          ops.PLAIN_SOFTMAX, self.noise, self.stops, prof_events=prof, row_base=self.row0,
+                          draft_row_stats=self.dstats if self.stash else None)
+
+    def __call__(self, prof=None):
+        self.draws()
+        return self.verify(prof)
+
+
+def row_counts(outs, _lib):
+    """(tokens, per-row accepted counts) of a list of VerifyOut (engine rule: no bonus token;
+    a reject adds the resampled token)."""
+    acc = torch.stack([o.n_accepted.long() for o in outs]).sum(0).cpu()
+    resid = sum(int(((o.row_status & _lib.SD_ROW_RESIDUAL) != 0).sum()) for o in outs)
+    return int(acc.sum()) + resid, acc
+
+
+def positive_rate_sums(acc_rows, drafted_per_row):
+    """engine/metrics.py:123-129 averages per-row acc/tot over the rows whose rate is > 0:
+    returns (Σ positive rates, count) so ranks can be summed."""
+    rates = acc_rows.double() / drafted_per_row
+    pos = rates[rates > 0]
+    return float(pos.sum()), int(pos.numel())
+
+
+def kernel_events(fn, repeat, n_pairs):
+    """Mean time of one `fn()` launch: torch events on the current stream (the one the ops launch
+    on) around `repeat` back-to-back launches, averaged over n_pairs pairs."""
+    ts = []
+    for _ in range(n_pairs):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(repeat):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / repeat)
+    return sum(ts) / len(ts)
 
 
 def main():
@@ -76,111 +186,88 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=dev)
 
-    import specdec_amd
+    import specdec_amd  # noqa: F401
     from specdec_amd import _lib, dp, ops
-    from specdec_amd.noise import PhiloxNoise
+    from specdec_amd.noise import PhiloxNoise, StreamNoise
 
-    # weak scaling: the global batch is args.batch rows per rank, split contiguously by row
-    # (specdec_amd/dp.py); Philox noise is keyed by the global row id, so the shards draw what
-    # one GPU verifying the whole batch would draw for the same rows.  No data-path collective.
     g, V = args.gamma, args.vocab
+    # weak scaling (the value): args.batch rows per rank, the global batch split contiguously by row
+    # (specdec_amd/dp.py); Philox noise is keyed by the global row id, so the shards draw what one GPU
+    # verifying the whole batch would draw for the same rows.  No data-path collective.
     row0, row1 = dp.shard_rows(args.batch * world, world, rank)
     B = row1 - row0
-    gen = torch.Generator(device=dev).manual_seed(1000 + rank)
-    tl = (torch.randn(B, g, V, generator=gen, device=dev) * 3.0).to(torch.bfloat16)
-    dl = (tl.float() + args.sigma * torch.randn(B, g, V, generator=gen, device=dev)).to(torch.bfloat16)
-    noise = PhiloxNoise(seed=4242)
-    draft = torch.empty(B, g, dtype=torch.long, device=dev)
-    dstats = torch.empty(g, B, 2, dtype=torch.float32, device=dev)   # drafter rows' (max, Σexp)
-    stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
-    trows = [tl[:, t, :] for t in range(g)]
-    drows = [dl[:, t, :] for t in range(g)]
-
-    def draws():
-        # engine/infer_engine.py:241-247: softmax + multinomial of each drafter row, one launch per
-        # draft position (in the engine a drafter forward sits between them)
-        for d in range(g):
-            ops.sample_rows(drows[d], ops.PLAIN_SOFTMAX, noise, tokens_out=draft[:, d], row_base=row0,
-                            row_stats_out=dstats[d])
-
-    def verify(prof=None):
-        return ops.verify(trows, drows, draft, _lib.SD_RULE_ENGINE, ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise,
-                          stops, prof_events=prof, row_base=row0, draft_row_stats=dstats)
-
-    def step(prof=None):
-        draws()
-        return verify(prof)
-
+    tl, dl = engine_logits(B, g, V, args.sigma, 1000 + rank, dev)
+    step = EngineStep(tl, dl, PhiloxNoise(seed=4242), row0, ops, _lib)
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps)
+    G = len(outs)
+    elapsed = timed_replays(graph, replays, dist)
 
-    # capture G steps per graph; K must be a multiple of G
-    G = max(1, min(args.graph_steps, args.steps))
-    while args.steps % G:
-        G -= 1
-    graph = torch.cuda.CUDAGraph()
-    outs = []
-    with torch.cuda.graph(graph):
-        for _ in range(G):
-            outs.append(step())
-    graph.replay()   # untimed warm replay
-    torch.cuda.synchronize()
-    replays = args.steps // G
+    # the verify alone (on the captured draws' outputs), for the per-phase breakdown
+    vgraph, _, _ = graph_steps(step.verify, args.steps, args.graph_steps)
+    verify_ms = timed_replays(vgraph, replays, None) / args.steps * 1e3
 
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(replays):
-        graph.replay()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    tokens_g, acc_rows = row_counts(outs, _lib)
+    rsum, rcnt = positive_rate_sums(acc_rows, g * G)
+    elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens_g * replays, "accepted": float(acc_rows.sum()) * replays,
+                                          "drafted": B * g * G * replays, "rate_sum": rsum, "rate_cnt": rcnt},
+                                dev, dist)
 
-    # the verify alone (same captured draws' outputs), for the per-phase breakdown
-    vgraph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(vgraph):
-        for _ in range(G):
-            verify()
-    vgraph.replay()
-    torch.cuda.synchronize()
-    tv = time.perf_counter()
-    for _ in range(replays):
-        vgraph.replay()
-    torch.cuda.synchronize()
-    verify_ms = (time.perf_counter() - tv) / args.steps * 1e3
-
-    # output tokens per replay (identical every replay: same inputs, same captured noise offsets)
-    acc = sum(int(o.n_accepted.sum()) for o in outs)
-    resid = sum(int(((o.row_status & _lib.SD_ROW_RESIDUAL) != 0).sum()) for o in outs)
-    tokens = (acc + resid) * replays
-    drafted = B * g * G * replays
-    elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens, "accepted": acc * replays, "drafted": drafted}, dev, dist)
-    tokens, accepted, drafted = tot["tokens"], tot["accepted"], tot["drafted"]
-
-    # dominant kernel: row statistics of the target rows.  HIP events on its stream
-    # around PROF_REPEAT back-to-back launches of it (sd_verify's prof_stats_repeat), so the
-    # event pair's own cost (~3-6 us, context dependent) is amortised; the per-launch figure
-    # still includes the launch-to-launch gaps, i.e. it errs on the slow side of rocprofv3's
-    # kernel-trace average (profiles/).
+    # per-kernel timing (HIP events on the launch stream, back-to-back launches so the event pair's
+    # own cost is amortised): k_draw (one per drafter draw), k_stats (sd_verify's prof hook, with its
+    # decide tail), and the rest of the verify (k_sample with its tail) by difference.
+    dgraph, _, _ = graph_steps(lambda: step.draw(0), PROF_REPEAT, PROF_REPEAT)   # launch-overhead free
+    draw_ms = kernel_events(dgraph.replay, 1, args.prof_steps) / PROF_REPEAT
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.prof_steps)]
     for e in ev:
         e[0].record()   # marks the torch events as recorded; sd_verify re-records them around k_stats
         e[1].record()
-        verify(prof=(e[0], e[1], PROF_REPEAT))
+        step.verify(prof=(e[0], e[1], PROF_REPEAT))
     torch.cuda.synchronize()
     stats_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev) / PROF_REPEAT
-    alg_bytes = B * g * V * 2               # k_stats: the γ target rows, once
-    achieved = alg_bytes / (stats_ms * 1e-3) / 1e9
+    sample_ms = max(verify_ms - stats_ms, 0.0)
     ms_per_step = elapsed / args.steps * 1e3
-    step_bytes = B * 2 * g * V * 2          # the step: every target and drafter row once
-    step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
+    row_bytes = B * V * 2
+    kernels = {
+        # per launch: algorithmic bytes = each logit row the kernel must read, once
+        "k_draw": {"ms": draw_ms, "launches_per_step": g, "alg_bytes_per_launch": row_bytes},
+        "k_stats": {"ms": stats_ms, "launches_per_step": 1, "alg_bytes_per_launch": g * row_bytes},
+        "k_sample": {"ms": sample_ms, "launches_per_step": 1, "alg_bytes_per_launch": 2 * row_bytes,
+                     "note": "verify minus k_stats (graph-timed); rows re-read from L2 / Infinity Cache"},
+    }
+    for k in kernels.values():
+        k["ms_per_step"] = k["ms"] * k["launches_per_step"]
+        k["achieved_gbs"] = k["alg_bytes_per_launch"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else None
+        k["frac"] = k["achieved_gbs"] / HBM_PEAK_GBS if k["achieved_gbs"] else None
+    dominant = max(kernels, key=lambda n: kernels[n]["ms_per_step"])
 
+    # strong scaling (configs[2] as written: a GLOBAL batch of args.batch rows split over the ranks)
+    strong = None
+    if world > 1:
+        s0, s1 = dp.shard_rows(args.batch, world, rank)
+        stl, sdl = tl[:s1 - s0], dl[:s1 - s0]
+        sstep = EngineStep(stl, sdl, PhiloxNoise(seed=4343), s0, ops, _lib)
+        for _ in range(max(args.warmup, 1)):
+            sstep()
+        torch.cuda.synchronize()
+        sgraph, souts, sreplays = graph_steps(sstep, args.steps, args.graph_steps)
+        selapsed = timed_replays(sgraph, sreplays, dist)
+        stoks, _ = row_counts(souts, _lib)
+        selapsed, stot = dp.aggregate(selapsed, {"tokens": stoks * sreplays}, dev, dist)
+        strong = {"value": stot["tokens"] / selapsed, "unit": "tokens/s", "global_batch": args.batch,
+                  "rows_per_gpu": s1 - s0, "ms_per_step": selapsed / args.steps * 1e3}
+
+    stream = None
+    if rank == 0 and args.stream_steps > 0:
+        stream = stream_line(tl, dl, row0, args, ops, _lib, StreamNoise)
+    cfg1 = None
+    if rank == 0 and world == 1 and not args.no_configs1:
+        cfg1 = configs1_lines(dev, args, ops, _lib, PhiloxNoise)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(tl, dl, draft, args)
+        cpu = cpu_baseline(tl, dl, step.draft, args)
 
     if rank == 0:
         traffic = None
@@ -188,12 +275,15 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 rec = json.load(f)
-            key = f"engine_drawstats_b{B}_g{g}_v{V}"
+            key = f"{dominant}_engine_b{B}_g{g}_v{V}"
             if key in rec:
                 traffic = rec[key]["hbm_bytes_per_launch"]
+        dk = kernels[dominant]
+        step_bytes = B * 2 * g * V * 2          # the step: every target and drafter row once
+        step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
         line = {
             "metric": METRIC,
-            "value": tokens / elapsed,
+            "value": tot["tokens"] / elapsed,
             "unit": "tokens/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -208,14 +298,21 @@ def main():
                                    "γ drafter draws + verify (rule A10)",
                        "rows_per_gpu": args.batch, "global_batch": args.batch * world, "gamma": g, "vocab": V,
                        "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G},
-            "acceptance_rate": accepted / drafted,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_stats", "kernel_ms": stats_ms, "launches_per_event_pair": PROF_REPEAT,
-                         "alg_bytes_per_launch": alg_bytes,
+            # engine/metrics.py:123-129: mean of per-row acc/tot over the rows with a positive rate
+            "acceptance_rate": tot["rate_sum"] / tot["rate_cnt"] if tot["rate_cnt"] else 0.0,
+            "acceptance_rate_pooled": tot["accepted"] / tot["drafted"],
+            "roofline": {"bound": "hbm", "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": dk["frac"], "traffic": traffic,
+                         "kernel": dominant, "kernel_ms": dk["ms"], "launches_per_step": dk["launches_per_step"],
+                         "launches_per_event_pair": PROF_REPEAT,
+                         "alg_bytes_per_launch": dk["alg_bytes_per_launch"],
                          "step_bytes": step_bytes, "step_achieved_gbs": step_gbs,
                          "step_frac": step_gbs / HBM_PEAK_GBS},
+            "kernels": kernels,
             "phases_ms": {"draws": ms_per_step - verify_ms, "verify": verify_ms},
+            "stream": stream,
+            "strong_scaling": strong,
+            "configs1": cfg1,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -223,21 +320,101 @@ def main():
         dist.destroy_process_group()
 
 
+def stream_line(tl, dl, row0, args, ops, _lib, StreamNoise):
+    """The same engine step in STREAM mode: the noise is the reference's own torch CPU generator
+    stream (bit-exact tokens under torch.manual_seed), eager steps (the generator is advanced
+    by the words each verify consumed)."""
+    gen = torch.Generator().manual_seed(1234)
+    step = EngineStep(tl, dl, StreamNoise(gen), row0, ops, _lib)
+    B, g = step.B, step.g
+    step()
+    torch.cuda.synchronize()
+    outs = []
+    t0 = time.perf_counter()
+    for _ in range(args.stream_steps):
+        outs.append(step())
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    tokens, acc_rows = row_counts(outs, _lib)
+    rsum, rcnt = positive_rate_sums(acc_rows, g * len(outs))
+    ms = dt / args.stream_steps * 1e3
+    return {"noise": "stream", "value": tokens / dt, "unit": "tokens/s", "ms_per_step": ms,
+            "steps": args.stream_steps, "rows": B, "acceptance_rate": rsum / rcnt if rcnt else 0.0,
+            "note": "torch CPU generator words (bit-exact with the reference), eager steps"}
+
+
+def configs1_lines(dev, args, ops, _lib, PhiloxNoise):
+    """configs[1]: batch 1, γ=4, rule A8 (sampling/speculative_decoding.py:105-187) over synthetic
+    Llama-3 shaped rows: γ drafter draws + one sd_verify over γ+1 target rows; greedy,
+    multinomial T=1 and nucleus top-p 0.9; hipGraph replays."""
+    g, V = args.gamma, args.vocab
+    tl, dl = engine_logits(1, g + 1, V, args.sigma, 11, dev)
+    dl = dl[:, :g].contiguous()
+    stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
+    trows = [tl[:, t] for t in range(g + 1)]
+    drows = [dl[:, t] for t in range(g)]
+    res = {}
+    for name, proc in (("greedy", ops.ProcSpec("greedy")), ("multinomial", ops.ProcSpec("multinomial", 1.0)),
+                       ("nucleus_p0.9", ops.ProcSpec("nucleus", 1.0, 0, 0.9))):
+        noise = PhiloxNoise(seed=7)
+        draft = torch.zeros(1, g, dtype=torch.long, device=dev)
+        dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev)
+
+        def step():
+            for d in range(g):
+                ops.sample_rows(drows[d], proc, noise, tokens_out=draft[:, d], row_stats_out=dstats[d])
+            return ops.verify(trows, drows, draft, _lib.SD_RULE_SPEC, proc, proc, noise, stops,
+                              draft_row_stats=dstats)
+
+        for _ in range(5):
+            step()
+        torch.cuda.synchronize()
+        graph, outs, replays = graph_steps(step, 200, 20)
+        dt = timed_replays(graph, replays, None)
+        n = torch.stack([o.n_accepted.long() for o in outs]).sum().item()
+        tokens = (n + len(outs)) * replays        # accepted + the resampled / bonus token, every step
+        res[name] = {"us_per_step": dt / (len(outs) * replays) * 1e6, "tokens_per_s": tokens / dt,
+                     "alg_bytes_per_step": (2 * g + 1) * V * 2}
+    return res
+
+
+def cpu_model_name():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for ln in out.splitlines():
+            if ln.startswith("Model name:"):
+                return ln.split(":", 1)[1].strip()
+    except Exception:
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for ln in f:
+                if ln.startswith("model name"):
+                    return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def cpu_baseline(tl, dl, draft, args):
     """Oracle (reference semantics, torch-CPU) on the same logits: the drafter draws
     (softmax + multinomial per draft position, engine/infer_engine.py:241-247), the target
-    softmax and the per-row accept/resample loop of :276-336."""
+    softmax and the per-row accept/resample loop of :276-336.  SURVEY §8(d): every host thread
+    this process may use (OMP_NUM_THREADS when the box sets it — its CPU share — else the
+    affinity mask), 3 warm-up steps, then the median of >= 20 steps (fewer only if a step takes
+    longer than args.cpu_seconds / 20)."""
     sys.path.insert(0, ROOT)
     from oracle import specdec_ref as ref
-    cores = min(len(os.sched_getaffinity(0)), 16)
+    cores = len(os.sched_getaffinity(0))
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        cores = min(cores, int(os.environ["OMP_NUM_THREADS"]))
     torch.set_num_threads(cores)
     tlc, dlc, dc = tl.cpu(), dl.cpu(), draft.cpu()
     B, g, V = tlc.shape
     gen_cpu = torch.Generator().manual_seed(0)
     noise = ref.TorchNoise(gen_cpu)
-    t0 = time.perf_counter()
-    steps = tokens = 0
-    while True:
+
+    def one_step():
         q = torch.softmax(dlc, dim=-1).float()
         for d in range(g):
             dc[:, d] = torch.multinomial(q[:, d], 1, generator=gen_cpu).squeeze(-1)
@@ -247,15 +424,24 @@ def cpu_baseline(tl, dl, draft, args):
         fin = torch.zeros(B, dtype=torch.bool)
         acc = torch.zeros(B, dtype=torch.long)
         n = ref.engine_verify_rows(p, q, dc, fin, [128001, 128009], 0, gen, acc, noise)
-        tokens += sum(min(k + 1, g) for k in n)
-        steps += 1
-        if time.perf_counter() - t0 > args.cpu_seconds:
+        return sum(min(k + 1, g) for k in n)
+
+    for _ in range(3):
+        one_step()
+    times, toks = [], []
+    t_all = time.perf_counter()
+    while len(times) < 20:
+        t0 = time.perf_counter()
+        toks.append(one_step())
+        times.append(time.perf_counter() - t0)
+        if len(times) >= 5 and time.perf_counter() - t_all > args.cpu_seconds:
             break
-    dt = time.perf_counter() - t0
-    return {"value": tokens / dt, "unit": "tokens/s", "cores": cores, "kind": "port",
-            "sample": f"{steps} engine steps (γ drafter draws + verify) of the same {B}x{g}x{V} bf16 logits "
-                      "(oracle, torch-CPU)",
-            "ms_per_step": dt / steps * 1e3}
+    med = statistics.median(times)
+    return {"value": (sum(toks) / len(toks)) / med, "unit": "tokens/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model_name(),
+            "sample": f"median of {len(times)} engine steps (after 3 warm-up) — γ drafter draws + verify of the "
+                      f"same {B}x{g}x{V} bf16 logits (oracle = reference semantics, torch-CPU, {cores} threads)",
+            "ms_per_step": med * 1e3}
 
 
 if __name__ == "__main__":

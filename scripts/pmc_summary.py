@@ -2,8 +2,9 @@
 
 Usage: python scripts/pmc_summary.py gpurun_out <tag> [workload_key]
 Writes profiles/<tag>_pmc_summary.csv (mean counter value per launch, per kernel) and, for
-the dominant kernel k_stats, profiles/pmc_traffic.json {workload_key: {...}} that bench.py
-reads for roofline.traffic.  HBM bytes follow the MI355X guide's gfx950 correction:
+each kernel family of the bench step (k_draw, k_stats, k_sample), profiles/pmc_traffic.json
+{"<family>_<workload_key>": {...}}; bench.py reads its dominant kernel's entry for
+roofline.traffic.  HBM bytes follow the MI355X guide's gfx950 correction:
 FETCH_SIZE / WRITE_SIZE are in KiB and FETCH_SIZE under-reports by 2x on gfx950.
 """
 from __future__ import annotations
@@ -48,21 +49,25 @@ def main():
             n = max(len(v) for v in d.values())
             w.writerow([kern, n] + [f"{sum(d[c]) / len(d[c]):.1f}" if d.get(c) else "" for c in ctrs])
     print(open(out).read())
-    # the bench's k_stats variant = the one launched most (the setup's draft sampling uses another)
-    stats = sorted((k for k in acc if k.startswith("sd::k_stats")),
-                   key=lambda k: -max(len(v) for v in acc[k].values()))
-    if stats:
-        d = acc[stats[0]]
+    # per kernel family (k_draw, k_stats, k_sample): the variant launched most is the bench's
+    # (setup launches use others); bench.py reads "<family>_<workload_key>" for roofline.traffic
+    pj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    rec = json.load(open(pj)) if os.path.exists(pj) else {}
+    for fam in ("k_draw", "k_stats", "k_sample"):
+        cands = sorted((k for k in acc if k.startswith("sd::" + fam + "<")),
+                       key=lambda k: -max(len(v) for v in acc[k].values()))
+        if not cands:
+            continue
+        d = acc[cands[0]]
         fetch = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"]) * 1024 * 2 if d.get("FETCH_SIZE") else None
         write = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"]) * 1024 if d.get("WRITE_SIZE") else 0.0
-        if fetch is not None:
-            pj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-            rec = json.load(open(pj)) if os.path.exists(pj) else {}
-            rec[key] = {"kernel": stats[0], "hbm_bytes_per_launch": fetch + write,
-                        "fetch_bytes": fetch, "write_bytes": write, "source": os.path.basename(out),
-                        "note": "FETCH_SIZE(KiB)*1024*2 (gfx950 correction) + WRITE_SIZE(KiB)*1024"}
-            json.dump(rec, open(pj, "w"), indent=1)
-            print(pj, rec[key])
+        if fetch is None:
+            continue
+        rec[f"{fam}_{key}"] = {"kernel": cands[0], "hbm_bytes_per_launch": fetch + write,
+                               "fetch_bytes": fetch, "write_bytes": write, "source": os.path.basename(out),
+                               "note": "FETCH_SIZE(KiB)*1024*2 (gfx950 correction) + WRITE_SIZE(KiB)*1024"}
+        print(fam, rec[f"{fam}_{key}"])
+    json.dump(rec, open(pj, "w"), indent=1)
 
 
 if __name__ == "__main__":

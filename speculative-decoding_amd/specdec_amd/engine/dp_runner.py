@@ -1,0 +1,136 @@
+"""Data-parallel runner for the drop-in engine: one process per GPU, the prompt batch split by row.
+
+The reference runs each prompt batch of engine/benchmark_executor.py:72-83 on one device
+(``infer_batch(runner, prompts)``).  Prompt rows are independent, so here every rank of a
+``torch.distributed`` job (one process per GPU; RCCL or gloo — only host objects are exchanged,
+after decoding) takes a contiguous row shard of the SAME tokenized global batch (the padding
+depends on the whole batch, so the batch is tokenized once, identically on every rank), runs
+``batch_speculative_generate`` on it with ``ctx.row_base`` = its first global row, and the
+per-row outputs / rates / request metrics are gathered in global row order.
+
+Under Philox noise the draws are keyed by (seed, call offset, GLOBAL row), so the gathered
+outputs equal those of one process decoding the whole batch (tests/test_dp_engine_gpu.py).
+There is no collective on the data path: the one exchange is ``all_gather_object`` of the
+finished rows' host results.
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional, Tuple
+
+import torch
+
+from .. import dp
+from .batch_decode import decode_batch_with_chat_template
+from .infer_engine import _fill_batch_metrics, batch_speculative_generate
+from .metrics import BatchMetrics
+
+
+def _world(dist) -> Tuple[int, int]:
+    if dist is None or not dist.is_initialized():
+        return 1, 0
+    return dist.get_world_size(), dist.get_rank()
+
+
+def _gather(obj, dist):
+    world, _ = _world(dist)
+    if world == 1:
+        return [obj]
+    out = [None] * world
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def batch_speculative_generate_dp(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor, dist=None,
+                                  first_token_callback=None) -> Tuple[List[torch.Tensor], List[float], float]:
+    """Decode the global batch [B, L] sharded over the ranks of `dist`.
+
+    Returns (outputs, rates, elapsed) for the WHOLE batch on every rank (outputs on this rank's
+    device, global row order) and this rank's decode wall time.  `first_token_callback` gets
+    GLOBAL row ids."""
+    world, rank = _world(dist)
+    B = input_ids.shape[0]
+    start, stop = dp.shard_rows(B, world, rank)
+    saved = getattr(ctx, "row_base", None)
+    ctx.row_base = start
+    cb = None if first_token_callback is None else (lambda i: first_token_callback(start + i))
+    err = None
+    outs, rates = [], []
+    t0 = time.time()
+    try:
+        if stop > start:
+            outs, rates = batch_speculative_generate(ctx, input_ids[start:stop], attention_mask[start:stop],
+                                                     stop - start, first_token_callback=cb)
+    except Exception as e:   # reported after the gather, so no rank is left waiting in it
+        err = f"rank {rank}: {type(e).__name__}: {e}"
+    finally:
+        if saved is None:
+            del ctx.row_base
+        else:
+            ctx.row_base = saved
+    elapsed = time.time() - t0
+    shards = _gather((err, [o.cpu() for o in outs], rates), dist)
+    errs = [s[0] for s in shards if s[0] is not None]
+    if errs:
+        raise RuntimeError("; ".join(errs))
+    dev = input_ids.device
+    outputs = [o.to(dev) for s in shards for o in s[1]]
+    all_rates = [r for s in shards for r in s[2]]
+    return outputs, all_rates, elapsed
+
+
+def run_batch_speculative_dp(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor, batch_size: int,
+                             dist=None) -> Optional[BatchMetrics]:
+    """engine/infer_engine.py:99-146 over the ranks: every rank returns the GLOBAL BatchMetrics
+    (requests in global row order; batch latency = the slowest rank's, i.e. the job's)."""
+    bm = BatchMetrics(batch_size=batch_size)
+    firsts: List[Optional[float]] = [None] * batch_size
+
+    def first_token(idx):
+        if idx < batch_size and firsts[idx] is None:
+            firsts[idx] = time.time()
+
+    ok = True
+    t_start = time.time()
+    try:
+        outputs, rates, _ = batch_speculative_generate_dp(ctx, input_ids, attention_mask, dist,
+                                                          first_token_callback=first_token)
+    except Exception as e:  # the reference's contract (:144-146); every rank must still join the gather
+        print(f"Batch speculative decoding failed: {type(e).__name__}: {e}")
+        ok, outputs, rates = False, [], []
+    t_end = time.time()
+    meta = _gather((ok, t_start, t_end, firsts), dist)
+    if not all(m[0] for m in meta):
+        return None
+    bm.batch_start_time = min(m[1] for m in meta)
+    bm.batch_end_time = max(m[2] for m in meta)
+    merged = [None] * batch_size
+    for m in meta:
+        for i, f in enumerate(m[3]):
+            if f is not None and merged[i] is None:
+                merged[i] = f
+    starts = [bm.batch_start_time] * batch_size
+    return _fill_batch_metrics(bm, outputs, attention_mask, starts, merged, rates)
+
+
+def infer_batch_dp(ctx, prompts: List[str], dist=None) -> Tuple[Optional[BatchMetrics], Optional[BatchMetrics]]:
+    """``infer_batch`` (engine/infer_engine.py:10-96) for a data-parallel job: same formatting and
+    tokenization of the whole prompt batch on every rank, then the row-sharded speculative run.
+    The target-only baseline is not sharded (it is outside the verify/accept path)."""
+    if not ctx.spec:
+        from .infer_engine import infer_batch
+        return infer_batch(ctx, prompts)
+    if ctx.chat:
+        formatted = [ctx.tokenizer.apply_chat_template([{"role": "user", "content": p}],
+                                                       add_generation_prompt=True, tokenize=False)
+                     for p in prompts]
+    else:
+        formatted = prompts
+    input_ids, attention_mask = decode_batch_with_chat_template(ctx.tokenizer, formatted,
+                                                                max_length=ctx.max_batch_length, chat=False)
+    drafter_device = getattr(ctx, "drafter_device", None)
+    if drafter_device is not None:
+        input_ids, attention_mask = input_ids.to(drafter_device), attention_mask.to(drafter_device)
+    if getattr(ctx, "reset_in_between", False) and getattr(ctx, "ngram", None) is not None:
+        ctx.ngram.reset()
+    return run_batch_speculative_dp(ctx, input_ids, attention_mask, len(prompts), dist), None

@@ -44,11 +44,37 @@ def infer_batch(ctx, prompts: List[str]) -> Tuple[Optional[BatchMetrics], Option
         input_ids, attention_mask = input_ids.to(drafter_device), attention_mask.to(drafter_device)
     if getattr(ctx, "reset_in_between", False) and getattr(ctx, "ngram", None) is not None:
         ctx.ngram.reset()
+    target_device = getattr(ctx, "target_device", None)
+    if not ctx.spec and getattr(ctx, "target_gen", False) and target_device is not None:
+        input_ids, attention_mask = input_ids.to(target_device), attention_mask.to(target_device)
     if ctx.spec:
         return run_batch_speculative(ctx, input_ids, attention_mask, len(prompts)), None
     if getattr(ctx, "target_gen", False):
-        raise NotImplementedError("target-only autoregressive decoding is outside the verify/accept path")
+        return None, run_batch_target(ctx, input_ids, attention_mask, len(prompts))
+    print("Warning: No inference method enabled")
     return None, None
+
+
+def _fill_batch_metrics(bm: BatchMetrics, outputs, attention_mask, starts, firsts, rates=None) -> BatchMetrics:
+    """engine/infer_engine.py:117-140 / :380-399: per-request metrics, the reference's formulas."""
+    prompt_tokens = attention_mask.sum(dim=1).tolist()
+    for i in range(bm.batch_size):
+        r = RequestMetrics()
+        r.start_time = starts[i]
+        r.prompt_tokens = int(prompt_tokens[i])
+        r.generated_tokens = len(outputs[i]) - r.prompt_tokens
+        r.total_tokens = len(outputs[i])
+        if rates is not None:
+            r.acceptance_rate = rates[i] if i < len(rates) else 0.0
+        r.end_time = bm.batch_end_time
+        if firsts[i] is not None:
+            r.first_token_time = firsts[i]
+            r.ttft = firsts[i] - starts[i]
+        else:
+            r.ttft = (bm.batch_end_time - starts[i]) / max(r.generated_tokens, 1)
+        r.total_latency = bm.batch_end_time - starts[i]
+        bm.requests.append(r)
+    return bm
 
 
 def run_batch_speculative(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor,
@@ -70,23 +96,81 @@ def run_batch_speculative(ctx, input_ids: torch.Tensor, attention_mask: torch.Te
         print(f"Batch speculative decoding failed: {type(e).__name__}: {e}")
         return None
     bm.batch_end_time = time.time()
-    prompt_tokens = attention_mask.sum(dim=1).tolist()
-    for i in range(batch_size):
-        r = RequestMetrics()
-        r.start_time = starts[i]
-        r.prompt_tokens = int(prompt_tokens[i])
-        r.generated_tokens = len(outputs[i]) - r.prompt_tokens
-        r.total_tokens = len(outputs[i])
-        r.acceptance_rate = rates[i] if i < len(rates) else 0.0
-        r.end_time = bm.batch_end_time
-        if firsts[i] is not None:
-            r.first_token_time = firsts[i]
-            r.ttft = firsts[i] - starts[i]
+    return _fill_batch_metrics(bm, outputs, attention_mask, starts, firsts, rates)
+
+
+def run_batch_target(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor,
+                     batch_size: int) -> Optional[BatchMetrics]:
+    """engine/infer_engine.py:362-404: the target-only baseline, same metrics rules."""
+    bm = BatchMetrics(batch_size=batch_size)
+    bm.batch_start_time = time.time()
+    starts = [time.time()] * batch_size
+    firsts: List[Optional[float]] = [None] * batch_size
+
+    def first_token(idx):
+        if idx < batch_size and firsts[idx] is None:
+            firsts[idx] = time.time()
+
+    try:
+        outputs = batch_autoregressive_generate(ctx, input_ids, attention_mask, batch_size,
+                                                first_token_callback=first_token)
+    except Exception as e:
+        print(f"Batch target generation failed: {type(e).__name__}: {e}")
+        return None
+    bm.batch_end_time = time.time()
+    return _fill_batch_metrics(bm, outputs, attention_mask, starts, firsts)
+
+
+@torch.no_grad()
+def batch_autoregressive_generate(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor, batch_size: int,
+                                  first_token_callback=None) -> List[torch.Tensor]:
+    """engine/infer_engine.py:407-497: target-only decoding, the baseline the benchmark compares
+    against (outside the verify/accept path, so plain torch ops on the device).
+
+    Same token rule: ``multinomial(softmax(logits / T))`` when the processor has T > 0, else
+    ``argmax(logits)``, over the rows still active; a row finishes on an end token; outputs are
+    the unpadded prompt + generated tokens up to the last nonzero one.  The reference gathers
+    and scatters per-row tuple caches for the active rows; here every row keeps its cache
+    position (the cache object is whatever the model returns) and only active rows' tokens are
+    taken, which gives the active rows the same logits.
+    """
+    dev = input_ids.device
+    gen_len = int(ctx.gen_len)
+    generated = torch.zeros(batch_size, gen_len, dtype=torch.long, device=dev)
+    finished = torch.zeros(batch_size, dtype=torch.bool, device=dev)
+    ends = torch.tensor(list(ctx.end_tokens), dtype=torch.long, device=dev)
+    temperature = float(getattr(ctx.processor, "temperature", 0.0) or 0.0)
+    past = None
+    for step in range(gen_len):
+        if bool(finished.all()):
+            break
+        if step == 0:
+            out = ctx.target(input_ids, attention_mask=attention_mask, use_cache=True)
         else:
-            r.ttft = (bm.batch_end_time - starts[i]) / max(r.generated_tokens, 1)
-        r.total_latency = bm.batch_end_time - starts[i]
-        bm.requests.append(r)
-    return bm
+            cur = generated[:, step - 1:step]
+            out = ctx.target(cur, attention_mask=torch.ones_like(cur), past_key_values=past, use_cache=True)
+        past = out.past_key_values
+        active = ~finished
+        logits = out.logits[:, -1, :][active]
+        if temperature > 0:
+            nxt = torch.multinomial(torch.softmax(logits / temperature, dim=-1), 1).squeeze(-1)
+        else:
+            nxt = torch.argmax(logits, dim=-1)
+        nxt = nxt.to(dev)
+        idx = torch.nonzero(active).flatten()
+        generated[idx, step] = nxt
+        if first_token_callback is not None and step == 0:
+            for i in idx.tolist():
+                first_token_callback(i)
+        finished[idx] |= torch.isin(nxt, ends)
+    outputs = []
+    gen_host = generated.cpu()
+    lens = attention_mask.sum(dim=1).tolist()
+    for i in range(batch_size):
+        nz = torch.nonzero(gen_host[i], as_tuple=True)[0]
+        tail = gen_host[i, :int(nz[-1]) + 1] if nz.numel() > 0 else torch.empty(0, dtype=torch.long)
+        outputs.append(torch.cat([input_ids[i][:int(lens[i])], tail.to(dev)]))
+    return outputs
 
 
 @torch.no_grad()
@@ -101,6 +185,9 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
     B = batch_size
     gen_len, gamma = int(ctx.gen_len), int(ctx.gamma)
     noise = default_noise()
+    # data-parallel shards (specdec_amd.engine.dp_runner): Philox noise is keyed by the GLOBAL row,
+    # so a shard starting at global row `row_base` draws what one process over the whole batch draws
+    row_base = int(getattr(ctx, "row_base", 0))
     generated = torch.zeros(B, gen_len, dtype=torch.long, device=dev)
     finished = torch.zeros(B, dtype=torch.uint8, device=dev)
     drafted = torch.zeros(B, dtype=torch.long, device=dev)
@@ -128,7 +215,7 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
             logits = out.logits[:, -1, :]
             past = out.past_key_values
             samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise,     # :241-246 softmax + multinomial
-                                        row_stats_out=dstats[d] if stash else None)
+                                        row_base=row_base, row_stats_out=dstats[d] if stash else None)
             rows.append(logits)
             draft_tokens[:, d] = torch.where(active, samples, draft_tokens[:, d])          # :252
             generated[:, step + d] = torch.where(active, samples, generated[:, step + d])  # :257
@@ -145,7 +232,7 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
         verify(trows, rows, draft_tokens, _lib.SD_RULE_ENGINE, PLAIN_SOFTMAX, PLAIN_SOFTMAX, noise, stops,
                active=active.to(torch.uint8),
                engine_state=dict(generated=generated, step=step, finished=finished, accepted=accepted),
-               draft_row_stats=dstats[:gw] if stash and t_logits.device == dev else None)
+               row_base=row_base, draft_row_stats=dstats[:gw] if stash and t_logits.device == dev else None)
         step += gw                                                        # :338
 
     gen_host = generated.cpu()

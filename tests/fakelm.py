@@ -26,8 +26,8 @@ class FakeCache:
     def get_seq_length(self) -> int:
         return self.length
 
-    def crop(self, max_length: int) -> None:   # transformers-5 DynamicCache.crop
-        self.length = max_length
+    def crop(self, max_length: int) -> None:   # transformers-5 DynamicCache.crop (negative: drop -k)
+        self.length = self.length + max_length if max_length < 0 else min(self.length, max_length)
 
 
 class FakeLM:
@@ -86,3 +86,28 @@ def likely_tokens(lm: FakeLM, rows: int = 12, top: int = 2, offset: int = 5):
     b = lm.bank.float().cpu()
     picks = torch.topk(b[offset:offset + rows], top, dim=-1).indices.reshape(-1).tolist()
     return sorted(set(int(t) for t in picks))
+
+
+class TupleFakeLM(FakeLM):
+    """FakeLM whose past_key_values is the legacy tuple-of-(K, V) layout [B, 1, L, 1] (one layer):
+    what the reference's target-only loop gathers / scatters per active row
+    (engine/infer_engine.py:430-467).  The cached length L sets the position offset.
+    no_cache=True: the model returns no cache at all (past_key_values None)."""
+
+    def __init__(self, bank, max_position_embeddings: int = 4096, pos_mult: int = 7, no_cache: bool = False):
+        super().__init__(bank, max_position_embeddings, pos_mult)
+        self.no_cache = no_cache
+
+    def __call__(self, input_ids=None, past_key_values=None, use_cache=False, attention_mask=None, **_):
+        ids = input_ids.to(self.bank.device)
+        B, L = ids.shape
+        off = 0
+        if isinstance(past_key_values, (tuple, list)) and len(past_key_values):
+            off = past_key_values[0][0].shape[2]
+        elif isinstance(past_key_values, FakeCache):
+            off = past_key_values.length
+        pos = torch.arange(off, off + L, device=ids.device, dtype=torch.long)
+        logits = self.bank[(ids * 31 + pos * self.pos_mult) % self.bank.shape[0]]
+        kv = torch.zeros(B, 1, off + L, 1, device=ids.device)
+        keep = use_cache and not self.no_cache
+        return SimpleNamespace(logits=logits, past_key_values=((kv, kv.clone()),) if keep else None)

@@ -13,6 +13,11 @@ banks of tests/fakelm.py under fixed ``torch.manual_seed`` seeds, and writes:
 * ``processors.safetensors`` — ``utils.logits_processor`` probabilities on small rows
 * ``caching.json``      — ``utils.caching.prune_tuple_cache`` shapes
 * ``ngram_loops.json``  — ``ngram_assisted.ngram_assisted_speculative_generate`` outputs (rule A11)
+* ``engine_surface.json`` — ``engine.metrics`` (``BenchmarkResults.to_dict`` and the printed
+  summaries of a fixed synthetic result set), ``engine.infer_engine.run_batch_speculative``'s
+  non-timing request fields and ``batch_autoregressive_generate`` outputs on FakeLM banks
+
+``python tests/golden/make_golden.py --only surface`` regenerates just the last file.
 
 Only data is committed (inputs are regenerated from seeds + checked by digest);
 no reference source travels.  The GPU box never runs this script.
@@ -224,5 +229,107 @@ def main():
         json.dump(shapes, f, indent=1)
 
 
+SURFACE_ENGINE_CASES = [
+    # name, V, dtype, B, gamma, gen_len, end_tokens, seed, pos_mult
+    ("rbs_b4_g4_fp32", 4096, "fp32", 4, 4, 24, [1], 0, 0),
+    ("rbs_b6_g4_fp32_eos", 2048, "fp32", 6, 4, 40, "likely", 1, 0),
+]
+SURFACE_AR_CASES = [
+    # name, V, dtype, B, gen_len, end_tokens, temperature, seed, cache ("none": the model returns no
+    # cache; "tuple": a growing tuple cache, which the reference's scatter cannot hold -> it raises)
+    ("ar_b3_greedy_fp32", 2048, "fp32", 3, 16, "likely", 0.0, 0, "none"),
+    ("ar_b4_multi_t07_fp32", 2048, "fp32", 4, 16, "likely", 0.7, 1, "none"),
+    ("ar_b2_greedy_bf16", 4096, "bf16", 2, 12, [1], 0.0, 2, "none"),
+    ("ar_b3_greedy_fp32_tuplecache", 2048, "fp32", 3, 8, [1], 0.0, 0, "tuple"),
+]
+
+
+def synthetic_results(metrics_mod):
+    """A fixed BenchmarkResults (two batches, one zero-rate request) built with `metrics_mod`'s
+    classes; the test builds the same object with the drop-in's classes."""
+    R, Bm, Res = metrics_mod.RequestMetrics, metrics_mod.BatchMetrics, metrics_mod.BenchmarkResults
+    out = {}
+    for method, scale in (("speculative", 1.0), ("target_ar", 1.7)):
+        res = Res(method=method, total_requests=5, total_batches=2, start_time=100.0, end_time=100.0 + 3.5 * scale)
+        for bi, sizes in enumerate(((11, 7, 13), (5, 9))):
+            b = Bm(batch_size=len(sizes), batch_start_time=100.0 + bi, batch_end_time=100.0 + bi + 1.25 * scale)
+            for ri, pt in enumerate(sizes):
+                r = R(prompt_tokens=pt, generated_tokens=3 * pt + ri, total_tokens=4 * pt + ri,
+                      ttft=0.01 * (ri + 1) * scale, total_latency=0.5 + 0.1 * ri * scale,
+                      acceptance_rate=0.0 if (bi, ri) == (0, 1) else 0.25 + 0.1 * ri + 0.05 * bi,
+                      drafts_generated=8 * pt, drafts_accepted=3 * pt)
+                b.requests.append(r)
+            res.batches.append(b)
+        out[method] = res
+    return out
+
+
+def make_surface():
+    """engine_surface.json: the benchmark-facing surface of the engine (metrics + run_batch_* +
+    the target-only baseline), from the reference itself."""
+    import contextlib
+    import io
+    _import_reference()
+    import engine.infer_engine as ie                                    # noqa
+    import engine.metrics as em                                         # noqa
+    from fakelm import TupleFakeLM
+    res = synthetic_results(em)
+    rec = {"to_dict": {k: v.to_dict() for k, v in res.items()}}
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        em.print_benchmark_summary(res["speculative"])
+        em.print_benchmark_summary(res["target_ar"])
+        em.print_comparison(res["speculative"], res["target_ar"])
+    rec["printed"] = buf.getvalue()
+
+    rbs = {}
+    for name, V, dt, B, gamma, gen_len, ends, seed, pos_mult in SURFACE_ENGINE_CASES:
+        target, drafter = make_pair(V, dtype=DT[dt], pos_mult=pos_mult)
+        if ends == "likely":
+            ends = likely_tokens(target)
+        ids = prompt_for(V, seed, batch=B)
+        mask = torch.ones_like(ids)
+        mask[0, :2] = 0      # a padded row: generated_tokens counts padding (:124-126)
+        ctx = SimpleNamespace(drafter=drafter, target=target, gamma=gamma, gen_len=gen_len, end_tokens=ends,
+                              target_device="cpu")
+        torch.manual_seed(seed)
+        bm = ie.run_batch_speculative(ctx, ids, mask, B)
+        rbs[name] = dict(vocab=V, dtype=dt, batch=B, gamma=gamma, gen_len=gen_len, end_tokens=ends, seed=seed,
+                         pos_mult=pos_mult, prompt=ids.tolist(), mask=mask.tolist(),
+                         target_digest=bank_digest(target), drafter_digest=bank_digest(drafter),
+                         requests=[dict(prompt_tokens=int(r.prompt_tokens), generated_tokens=int(r.generated_tokens),
+                                        total_tokens=int(r.total_tokens), acceptance_rate=float(r.acceptance_rate))
+                                   for r in bm.requests])
+        print(name, [r["generated_tokens"] for r in rbs[name]["requests"]], flush=True)
+    rec["run_batch_speculative"] = rbs
+
+    ar = {}
+    for name, V, dt, B, gen_len, ends, T, seed, cache in SURFACE_AR_CASES:
+        target, _ = make_pair(V, dtype=DT[dt], pos_mult=3)
+        if ends == "likely":
+            ends = likely_tokens(target)
+        tl = TupleFakeLM(target.bank, pos_mult=3, no_cache=cache == "none")
+        ids = prompt_for(V, seed, batch=B)
+        mask = torch.ones_like(ids)
+        ctx = SimpleNamespace(target=tl, gen_len=gen_len, end_tokens=ends, processor=SimpleNamespace(temperature=T))
+        torch.manual_seed(seed)
+        rec_ar = dict(vocab=V, dtype=dt, batch=B, gen_len=gen_len, end_tokens=ends, temperature=T, seed=seed,
+                      cache=cache, prompt=ids.tolist(), target_digest=bank_digest(target))
+        try:
+            outs = ie.batch_autoregressive_generate(ctx, ids, mask, B)
+            rec_ar.update(outputs=[o.tolist() for o in outs], raised=None)
+        except Exception as e:
+            rec_ar.update(outputs=None, raised=f"{type(e).__name__}: {e}")
+        ar[name] = rec_ar
+        print(name, rec_ar["raised"] or [len(o) for o in rec_ar["outputs"]], flush=True)
+    rec["batch_autoregressive_generate"] = ar
+    with open(os.path.join(HERE, "engine_surface.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+
+
 if __name__ == "__main__":
-    main()
+    if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "surface":
+        make_surface()
+    else:
+        main()
+        make_surface()

@@ -1,0 +1,110 @@
+"""Drop-in engine surface on the GPU:
+
+* run_batch_speculative's non-timing request fields (prompt / generated / total tokens,
+  acceptance rate) equal the reference's own run_batch_speculative on the same FakeLM banks and
+  seed (tests/golden/engine_surface.json; STREAM noise = the reference's torch CPU draws), and
+  the BatchMetrics feed BenchmarkResults.to_dict;
+* the data-parallel runner (specdec_amd.engine.dp_runner): two processes (gloo, both on cuda:0 —
+  the GPU box has one card) decoding row shards of one batch under Philox noise return exactly
+  what one process decoding the whole batch returns.
+"""
+import json
+import os
+import socket
+from types import SimpleNamespace
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from fakelm import make_pair
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+with open(os.path.join(HERE, "golden", "engine_surface.json")) as f:
+    GOLD = json.load(f)
+DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
+DEV = "cuda"
+
+
+@pytest.mark.parametrize("case", sorted(GOLD["run_batch_speculative"]))
+def test_run_batch_speculative_fields_match_reference(case):
+    from specdec_amd import set_noise_mode
+    from specdec_amd.engine import metrics as em
+    from specdec_amd.engine.infer_engine import run_batch_speculative
+    c = GOLD["run_batch_speculative"][case]
+    set_noise_mode("stream")
+    target, drafter = make_pair(c["vocab"], dtype=DT[c["dtype"]], device=DEV, pos_mult=c["pos_mult"])
+    ids = torch.tensor(c["prompt"], dtype=torch.long, device=DEV)
+    mask = torch.tensor(c["mask"], dtype=torch.long, device=DEV)
+    ctx = SimpleNamespace(drafter=drafter, target=target, gamma=c["gamma"], gen_len=c["gen_len"],
+                          end_tokens=c["end_tokens"])
+    torch.manual_seed(c["seed"])
+    bm = run_batch_speculative(ctx, ids, mask, c["batch"])
+    assert bm is not None
+    got = [dict(prompt_tokens=r.prompt_tokens, generated_tokens=r.generated_tokens, total_tokens=r.total_tokens,
+                acceptance_rate=r.acceptance_rate) for r in bm.requests]
+    assert got == c["requests"]
+    d = em.BenchmarkResults(method="speculative", batches=[bm], start_time=bm.batch_start_time,
+                            end_time=bm.batch_end_time).to_dict()
+    assert d["total_tokens"] == sum(r["generated_tokens"] for r in c["requests"])
+    assert all(r["ttft"] >= 0 for r in d["batches"][0]["requests"])
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _decode_setup(V=4096, B=6):
+    target, drafter = make_pair(V, dtype=torch.bfloat16, device=DEV, pos_mult=0)
+    g = torch.Generator().manual_seed(4321)
+    ids = torch.randint(3, V, (B, 8), generator=g).to(DEV)
+    ctx = SimpleNamespace(drafter=drafter, target=target, gamma=4, gen_len=24, end_tokens=[1])
+    return ctx, ids
+
+
+def _dp_worker(rank, world, port, seed, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from specdec_amd import set_noise_mode
+        from specdec_amd.engine.dp_runner import batch_speculative_generate_dp, run_batch_speculative_dp
+        ctx, ids = _decode_setup()
+        set_noise_mode("philox", seed=seed)
+        outs, rates, _ = batch_speculative_generate_dp(ctx, ids, torch.ones_like(ids), dist)
+        set_noise_mode("philox", seed=seed)
+        bm = run_batch_speculative_dp(ctx, ids, torch.ones_like(ids), ids.shape[0], dist)
+        if rank == 0:
+            out.put(([o.cpu().tolist() for o in outs], rates,
+                     [(r.generated_tokens, r.acceptance_rate) for r in bm.requests]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_runner_two_ranks_equal_one_process():
+    from specdec_amd import set_noise_mode
+    from specdec_amd.engine.infer_engine import batch_speculative_generate
+    seed = 9090
+    ctx, ids = _decode_setup()
+    set_noise_mode("philox", seed=seed)
+    want, wrates = batch_speculative_generate(ctx, ids, torch.ones_like(ids), ids.shape[0])
+    want = [o.cpu().tolist() for o in want]
+    set_noise_mode("stream")
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_dp_worker, args=(r, 2, port, seed, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, rates, reqs = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want and rates == wrates
+    assert [g for g, _ in reqs] == [len(o) - ids.shape[1] for o in want]
+    assert [a for _, a in reqs] == wrates
