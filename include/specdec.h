@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 4
+#define SD_ABI_VERSION 5
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -323,6 +323,51 @@ int32_t sd_ngram_store_has_gram(const sd_ngram_store* store, const int64_t* ngra
 /* Host side: torch CPU generator state (torch.Generator.get_state(), 5056 bytes) <-> words. */
 int32_t sd_mt19937_fill(const uint8_t* torch_state, size_t state_len, uint32_t* out, int64_t n);
 int32_t sd_mt19937_advance(uint8_t* torch_state, size_t state_len, int64_t n);
+
+/* ---- STREAM noise generated on the device (csrc/mt_device.hip, csrc/mt_jump.cpp) ----------------
+ * The same words as sd_mt19937_fill, produced by the GPU: the generator state lives in device
+ * memory as an sd_mt_state (the current 624-word block of untempered words and the position tau0
+ * in [0, 624] of the next word to consume; tau0 = 624 means the next word starts a new block).
+ * sd_mt19937_generate writes the next n words (tempered, as torch.rand / exponential_ read them)
+ * WITHOUT moving the state; sd_mt19937_commit then moves it past the words a consumer used — a
+ * host count, or the device int64 a verify kernel wrote to words_used (no host sync).  A fill is
+ * cut into substreams of stride_words words; substream s >= 1 starts at a jump of s*stride_words
+ * words, given by jump polynomial s-1 of a table from sd_mt19937_jump_table (host; copy it to the
+ * device once per stride).  Replaces the host-thread generation behind torch.rand
+ * (sampling/speculative_decoding.py:139, engine/infer_engine.py:305) and torch.multinomial's
+ * Exp(1) noise (utils/logits_processor.py:48-49, engine/infer_engine.py:246,322-324). */
+#define SD_MT_JUMP_WORDS 320   /* uint64 per jump polynomial (degree < 19937, zero-padded)        */
+#define SD_MT_JUMP_CHUNKS 16   /* polynomial bit chunks per jump (one wave each)                 */
+
+typedef struct {
+    uint32_t mt[624];      /* the current block x[624 b .. 624 b + 623], untempered               */
+    int32_t tau0;          /* next word = x[624 b + tau0]; 624: the next word starts block b + 1   */
+    int32_t reserved[3];
+} sd_mt_state;
+
+typedef struct {
+    sd_mt_state* state;          /* device                                                     */
+    const uint64_t* jump_table;  /* device, jump_count * SD_MT_JUMP_WORDS                     */
+    int32_t jump_count;          /* >= ceil(n_words / stride_words) - 1                       */
+    int64_t stride_words;        /* >= 624; the table's stride                                */
+    uint32_t* words;             /* device out, n_words                                      */
+    int64_t n_words;
+    void* workspace;             /* device, sd_mt19937_generate_workspace_size bytes          */
+    size_t workspace_bytes;
+} sd_mt_generate_args;
+
+/* host */
+int32_t sd_mt19937_state_from_torch(const uint8_t* torch_state, size_t state_len, sd_mt_state* out);
+int32_t sd_mt19937_state_to_torch(const sd_mt_state* state, uint8_t* torch_state, size_t state_len);
+int32_t sd_mt19937_jump_table(int64_t stride_words, int32_t count, uint64_t* out);  /* count * SD_MT_JUMP_WORDS */
+int32_t sd_mt19937_char_poly(uint64_t* out, size_t words);                         /* >= 313 words           */
+int32_t sd_mt19937_fill_substreams(const uint32_t* block, int32_t tau0, uint32_t* out, int64_t n,
+                                   int64_t stride_words, const uint64_t* table, int32_t count);
+/* device */
+size_t sd_mt19937_generate_workspace_size(int64_t n_words, int64_t stride_words);
+int32_t sd_mt19937_generate(const sd_mt_generate_args* args, void* stream);
+int32_t sd_mt19937_commit(sd_mt_state* state, const uint32_t* words, int64_t n_words, const int64_t* used_dev,
+                          int64_t used, int32_t* status, void* stream);
 
 #ifdef __cplusplus
 }

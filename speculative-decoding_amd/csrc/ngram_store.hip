@@ -53,6 +53,24 @@ __device__ __forceinline__ bool gram_key(const int64_t* seq, int64_t e, int j, i
     return true;
 }
 
+// gram_key over the last j of C register-held ids (ctx[C-1] newest): static indices only, so
+// the ids stay in registers (a runtime index into ctx[] put them in scratch)
+template <int C>
+__device__ __forceinline__ bool gram_key_ctx(const int64_t (&ctx)[C], int j, uint64_t& key) {
+    uint64_t k = kUsed | ((uint64_t)j << 51);
+    bool ok = true;
+#pragma unroll
+    for (int t = 0; t < C; ++t) {
+        if (t >= C - j) {
+            const int64_t v = ctx[t];
+            ok &= v >= 0 && v <= (int64_t)kTokMask;
+            k |= (uint64_t)(v & kTokMask) << (kTokBits * (t - (C - j)));
+        }
+    }
+    key = k;
+    return ok;
+}
+
 // slot of key (inserted when absent if INSERT), -1 when absent (lookup) or the table is full
 template <bool INSERT>
 __device__ __forceinline__ int64_t probe(uint64_t* keys, int64_t cap, uint64_t key, int32_t* status) {
@@ -202,7 +220,7 @@ __global__ void __launch_bounds__(kThreads) k_ng_draft(sd_ngram_store S, const i
         uint8_t kn = 0;
         for (int j = hi; j >= lo && j >= 1; --j) {
             uint64_t gk;
-            if (!gram_key(ctx, C, j, j, gk)) break;
+            if (!gram_key_ctx(ctx, j, gk)) break;
             const int64_t gs = probe<false>(S.gram_keys, S.gram_capacity, gk, S.status);
             if (gs < 0) continue;
             const uint64_t best = S.gram_best[gs];

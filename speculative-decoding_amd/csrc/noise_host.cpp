@@ -72,6 +72,29 @@ int32_t sd_mt19937_fill(const uint8_t* torch_state, size_t state_len, uint32_t* 
     return SD_OK;
 }
 
+/* torch state <-> the device generator's block + position (sd_mt_state, csrc/mt_device.hip).
+ * torch twists lazily: left == 1 means the next word starts a new block (tau0 = 624); otherwise
+ * the next word is state[next] and left == 625 - next. */
+int32_t sd_mt19937_state_from_torch(const uint8_t* torch_state, size_t state_len, sd_mt_state* out) {
+    Mt m;
+    if (!out || !load(m, torch_state, state_len)) return SD_ERR_INVALID;
+    if (m.left != 1 && m.left + (int32_t)m.next != kN + 1) return SD_ERR_INVALID;
+    std::memcpy(out->mt, m.st, sizeof(m.st));
+    out->tau0 = m.left == 1 ? kN : (int32_t)m.next;
+    out->reserved[0] = out->reserved[1] = out->reserved[2] = 0;
+    return SD_OK;
+}
+
+int32_t sd_mt19937_state_to_torch(const sd_mt_state* st, uint8_t* torch_state, size_t state_len) {
+    Mt m;
+    if (!st || !load(m, torch_state, state_len) || st->tau0 < 1 || st->tau0 > kN) return SD_ERR_INVALID;
+    std::memcpy(m.st, st->mt, sizeof(m.st));
+    m.next = (uint32_t)st->tau0;
+    m.left = kN + 1 - st->tau0;
+    store(m, torch_state);
+    return SD_OK;
+}
+
 int32_t sd_mt19937_advance(uint8_t* torch_state, size_t state_len, int64_t n) {
     Mt m;
     if (!load(m, torch_state, state_len) || n < 0) return SD_ERR_INVALID;

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 4
+SD_ABI_VERSION = 5
 SD_MAX_GAMMA = 16
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
@@ -35,7 +35,14 @@ EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify
            "sd_sample_workspace_size", "sd_sample", "sd_probs_workspace_size", "sd_probs",
            "sd_ngram_workspace_size", "sd_ngram_verify", "sd_mt19937_fill", "sd_mt19937_advance",
            "sd_ngram_store_initialize", "sd_ngram_store_update", "sd_ngram_store_next_token",
-           "sd_ngram_store_has_gram", "sd_ngram_store_draft")
+           "sd_ngram_store_has_gram", "sd_ngram_store_draft",
+           "sd_mt19937_state_from_torch", "sd_mt19937_state_to_torch", "sd_mt19937_jump_table",
+           "sd_mt19937_char_poly", "sd_mt19937_fill_substreams", "sd_mt19937_generate_workspace_size",
+           "sd_mt19937_generate", "sd_mt19937_commit")
+
+SD_MT_JUMP_WORDS = 320
+SD_MT_JUMP_CHUNKS = 16
+SD_MT_STATE_BYTES = 624 * 4 + 16
 
 
 SD_NGRAM_MAX_N = 4
@@ -48,6 +55,16 @@ class sd_ngram_store(C.Structure):
                 ("pair_keys", C.c_void_p), ("pair_count", C.c_void_p), ("pair_ts", C.c_void_p),
                 ("pair_capacity", C.c_int64), ("status", C.c_void_p), ("n", C.c_int32), ("one_level", C.c_int32),
                 ("vocab", C.c_int32)]
+
+
+class sd_mt_state(C.Structure):
+    _fields_ = [("mt", C.c_uint32 * 624), ("tau0", C.c_int32), ("reserved", C.c_int32 * 3)]
+
+
+class sd_mt_generate_args(C.Structure):
+    _fields_ = [("state", C.c_void_p), ("jump_table", C.c_void_p), ("jump_count", C.c_int32),
+                ("stride_words", C.c_int64), ("words", C.c_void_p), ("n_words", C.c_int64),
+                ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t)]
 
 
 class sd_processor(C.Structure):
@@ -162,6 +179,19 @@ def _load():
     lib.sd_mt19937_fill.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_int64]
     lib.sd_mt19937_advance.restype = C.c_int32
     lib.sd_mt19937_advance.argtypes = [C.c_void_p, C.c_size_t, C.c_int64]
+    for name, res, args in (
+            ("sd_mt19937_state_from_torch", C.c_int32, [C.c_void_p, C.c_size_t, C.c_void_p]),
+            ("sd_mt19937_state_to_torch", C.c_int32, [C.c_void_p, C.c_void_p, C.c_size_t]),
+            ("sd_mt19937_jump_table", C.c_int32, [C.c_int64, C.c_int32, C.c_void_p]),
+            ("sd_mt19937_char_poly", C.c_int32, [C.c_void_p, C.c_size_t]),
+            ("sd_mt19937_fill_substreams", C.c_int32, [C.c_void_p, C.c_int32, C.c_void_p, C.c_int64, C.c_int64,
+                                                        C.c_void_p, C.c_int32]),
+            ("sd_mt19937_generate_workspace_size", C.c_size_t, [C.c_int64, C.c_int64]),
+            ("sd_mt19937_generate", C.c_int32, [C.POINTER(sd_mt_generate_args), C.c_void_p]),
+            ("sd_mt19937_commit", C.c_int32, [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p,
+                                              C.c_void_p])):
+        getattr(lib, name).restype = res
+        getattr(lib, name).argtypes = args
     P = C.POINTER(sd_ngram_store)
     for name, args in (("sd_ngram_store_initialize", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_void_p]),
                        ("sd_ngram_store_update", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_int32,

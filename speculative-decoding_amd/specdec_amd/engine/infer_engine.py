@@ -23,7 +23,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import _lib
-from ..noise import PhiloxNoise, default_noise
+from ..noise import PhiloxNoise, default_noise, noise_session
 from ..ops import PLAIN_SOFTMAX, sample_rows, verify
 from .batch_decode import decode_batch_with_chat_template
 from .metrics import BatchMetrics, RequestMetrics
@@ -181,10 +181,16 @@ def batch_speculative_generate(ctx, input_ids: torch.Tensor, attention_mask: tor
     if dev.type != "cuda":
         raise RuntimeError("specdec_amd.batch_speculative_generate runs on the GPU (HIP); input_ids are on "
                            f"{dev}. There is no CPU path.")
+    noise = default_noise()
+    with noise_session(noise):   # STREAM: the generator state stays on the device for the loop
+        return _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_size, first_token_callback)
+
+
+def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_size, first_token_callback):
+    dev = input_ids.device
     target_device = getattr(ctx, "target_device", dev)
     B = batch_size
     gen_len, gamma = int(ctx.gen_len), int(ctx.gamma)
-    noise = default_noise()
     # data-parallel shards (specdec_amd.engine.dp_runner): Philox noise is keyed by the GLOBAL row,
     # so a shard starting at global row `row_base` draws what one process over the whole batch draws
     row_base = int(getattr(ctx, "row_base", 0))

@@ -3,8 +3,10 @@
 StreamNoise  (parity mode)  feeds the kernels the raw mt19937 words of torch's CPU generator
              (torch.default_generator unless one is given), so every torch.rand / multinomial
              draw the reference makes is reproduced bit-exactly, in the reference's order, on
-             the GPU.  Words are generated on the host by libspecdec (sd_mt19937_fill) and the
-             generator is advanced by exactly the words the kernels consumed.
+             the GPU.  The words are made ON THE GPU from the generator's state
+             (sd_mt19937_generate: jump-ahead substreams, csrc/mt_device.hip) and the state is
+             moved by exactly the words the kernels consumed (sd_mt19937_commit, device-side
+             count); SPECDEC_STREAM_DEVICE=0 makes them on the host instead (sd_mt19937_fill).
 PhiloxNoise  (perf mode)    counter-based Philox4x32-10 inside the kernels: no host work, no
              noise bytes in HBM; statistically equivalent, not stream-identical.
 
@@ -13,8 +15,10 @@ SPECDEC_NOISE environment variable (``stream`` | ``philox``; default ``stream``)
 """
 from __future__ import annotations
 
+import contextlib
+import ctypes as C
 import os
-from typing import Optional
+from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
@@ -23,18 +27,101 @@ from . import _lib
 from ._lib import lib
 
 
+_DEVICE_GEN = os.environ.get("SPECDEC_STREAM_DEVICE", "1") != "0"
+MT_STRIDE = int(os.environ.get("SPECDEC_MT_STRIDE", "65536"))   # words per device substream
+_JUMP: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+
+
+def jump_table(device, stride: int, count: int) -> torch.Tensor:
+    """Device copy of the jump polynomials for substreams 1..>=count of `stride` words (host
+    computed once by libspecdec, grown geometrically)."""
+    dev = torch.device(device)
+    key = (dev, stride)
+    t = _JUMP.get(key)
+    if t is None or t.shape[0] < count:
+        n = max(count, 2 * (t.shape[0] if t is not None else 0), 16)
+        host = np.zeros((n, _lib.SD_MT_JUMP_WORDS), dtype=np.uint64)
+        _lib.check(lib.sd_mt19937_jump_table(stride, n, host.ctypes.data), "sd_mt19937_jump_table")
+        t = torch.from_numpy(host.view(np.int64)).to(dev)
+        _JUMP[key] = t
+    return t
+
+
+class _DeviceMT:
+    """The generator state on one device (sd_mt_state) plus the word buffer and workspace of the
+    last fill.  Fills and commits are stream-ordered; nothing here syncs except pull()."""
+
+    def __init__(self, device, torch_state: torch.Tensor):
+        self.device = torch.device(device)
+        host = _lib.sd_mt_state()
+        st = torch_state.contiguous()
+        _lib.check(lib.sd_mt19937_state_from_torch(st.data_ptr(), st.numel(), C.byref(host)),
+                   "sd_mt19937_state_from_torch")
+        raw = np.frombuffer(bytes(host), dtype=np.uint8).copy()
+        self.state = torch.from_numpy(raw).to(self.device)
+        self.words = torch.empty(0, dtype=torch.int32, device=self.device)
+        self.ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.n_generated = 0
+
+    def fill(self, n_words: int) -> torch.Tensor:
+        """The next n_words words (plus one block of slack for the commit), state unchanged."""
+        n = max(int(n_words), 1) + 624
+        if self.words.numel() < n:
+            self.words = torch.empty(n + n // 4, dtype=torch.int32, device=self.device)
+        S = (n + MT_STRIDE - 1) // MT_STRIDE
+        table = jump_table(self.device, MT_STRIDE, max(S - 1, 1))
+        need = lib.sd_mt19937_generate_workspace_size(n, MT_STRIDE)
+        if self.ws.numel() < need:
+            self.ws = torch.empty(need + need // 4, dtype=torch.uint8, device=self.device)
+        a = _lib.sd_mt_generate_args(self.state.data_ptr(), table.data_ptr(), table.shape[0], MT_STRIDE,
+                                     self.words.data_ptr(), n, self.ws.data_ptr(), self.ws.numel())
+        _lib.check(lib.sd_mt19937_generate(C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "sd_mt19937_generate")
+        self.n_generated = n
+        return self.words[:n]
+
+    def commit(self, count: Optional[int] = None, used_dev: Optional[torch.Tensor] = None) -> None:
+        used_ptr = used_dev.data_ptr() if used_dev is not None else None
+        _lib.check(lib.sd_mt19937_commit(self.state.data_ptr(), self.words.data_ptr(), self.n_generated, used_ptr,
+                                         int(count or 0), None,
+                                         C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
+                   "sd_mt19937_commit")
+
+    def pull(self, gen: torch.Generator) -> None:
+        """Write the device state back into the torch generator (one device->host copy)."""
+        host = _lib.sd_mt_state.from_buffer_copy(self.state.cpu().numpy().tobytes())
+        st = gen.get_state().clone()
+        _lib.check(lib.sd_mt19937_state_to_torch(C.byref(host), st.data_ptr(), st.numel()),
+                   "sd_mt19937_state_to_torch")
+        gen.set_state(st)
+
+
 class StreamNoise:
+    """Parity noise: torch's CPU generator words (torch.default_generator unless one is given).
+
+    device_generation (default on; SPECDEC_STREAM_DEVICE=0 turns it off): the words are made on
+    the GPU by libspecdec's mt19937 kernels from the generator's state, and the state moves on
+    the device by exactly the words the kernels consumed.  Outside a ``session`` every call loads
+    the generator state, and writes the moved state back after the call (one host round trip per
+    call, as the host path).  Inside ``with noise.session(device):`` the state stays on the device
+    across calls (no host syncs) and is written back to the generator when the session ends —
+    nothing else may draw from the generator meanwhile.
+    """
     mode = _lib.SD_NOISE_STREAM
 
-    def __init__(self, generator: Optional[torch.Generator] = None):
+    def __init__(self, generator: Optional[torch.Generator] = None, device_generation: Optional[bool] = None):
         self.generator = generator
+        self.device_generation = _DEVICE_GEN if device_generation is None else bool(device_generation)
+        self._dev: Optional[_DeviceMT] = None
+        self._depth = 0
 
     @property
     def gen(self) -> torch.Generator:
         return self.generator if self.generator is not None else torch.default_generator
 
+    # ---- host path -------------------------------------------------------------------------
     def draw(self, n_words: int, device) -> torch.Tensor:
-        """The next n_words generator words (the generator is NOT advanced), on `device`."""
+        """The next n_words generator words made on the HOST (the generator is NOT advanced)."""
         n = max(int(n_words), 1)
         st = self.gen.get_state().contiguous()
         host = np.empty(n, dtype=np.uint32)
@@ -47,6 +134,40 @@ class StreamNoise:
         st = self.gen.get_state().clone()
         _lib.check(lib.sd_mt19937_advance(st.data_ptr(), st.numel(), int(n_words)), "sd_mt19937_advance")
         self.gen.set_state(st)
+
+    # ---- the kernels' interface (ops.py) -----------------------------------------------------
+    def prepare(self, n_words: int, device) -> torch.Tensor:
+        """Device words for a call that may consume up to n_words words."""
+        dev = torch.device(device)
+        if not self.device_generation or dev.type != "cuda":
+            return self.draw(n_words, dev)
+        if self._dev is None or self._dev.device != dev:
+            if self._dev is not None:                   # moving devices mid-session: hand over
+                self._dev.pull(self.gen)
+            self._dev = _DeviceMT(dev, self.gen.get_state())
+        return self._dev.fill(n_words)
+
+    def consumed(self, count: Optional[int] = None, used_dev: Optional[torch.Tensor] = None) -> None:
+        """The call consumed `count` words (or the device int64 `used_dev` holds the count)."""
+        if self._dev is None:
+            self.advance(int(used_dev.item()) if used_dev is not None else int(count or 0))
+            return
+        self._dev.commit(count, used_dev)
+        if self._depth == 0:
+            self._dev.pull(self.gen)
+            self._dev = None
+
+    @contextlib.contextmanager
+    def session(self):
+        """Keep the generator state on the device across calls (see the class docstring)."""
+        self._depth += 1
+        try:
+            yield self
+        finally:
+            self._depth -= 1
+            if self._depth == 0 and self._dev is not None:
+                self._dev.pull(self.gen)
+                self._dev = None
 
 
 class PhiloxNoise:
@@ -83,3 +204,9 @@ def default_noise():
             _philox = PhiloxNoise()
         return _philox
     return StreamNoise()
+
+
+def noise_session(noise):
+    """``noise.session()`` for StreamNoise (state kept on the device for a whole decode loop),
+    a no-op context for PhiloxNoise."""
+    return noise.session() if isinstance(noise, StreamNoise) else contextlib.nullcontext()

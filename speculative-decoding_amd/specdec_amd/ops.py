@@ -2,7 +2,8 @@
 
 Every call validates shapes, strides and dtypes on the host BEFORE a kernel is enqueued,
 then launches on the current HIP stream of the tensors' device.  Nothing here syncs except
-where noted (StreamNoise needs the consumed word count to advance the torch generator).
+where noted: StreamNoise outside a ``session`` writes the moved generator state back to the
+torch generator after each call (one device->host copy).
 """
 from __future__ import annotations
 
@@ -90,7 +91,7 @@ def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
     """(sd_noise, keepalive tensor) for a call that may consume up to n_words_needed words.
     row_base: global id of the call's row 0 (Philox noise is keyed by the global row)."""
     if isinstance(noise, StreamNoise):
-        words = noise.draw(n_words_needed, device)
+        words = noise.prepare(n_words_needed, device)
         return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0, 0), words
     if isinstance(noise, PhiloxNoise):
         if not 0 <= row_base < (1 << 24):
@@ -133,7 +134,7 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
                             row_stats_out.data_ptr() if row_stats_out is not None else None)
     _lib.check(lib.sd_sample(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_sample")
     if isinstance(noise, StreamNoise):
-        noise.advance(need)
+        noise.consumed(count=need)
     del keep
     return tokens, prob, status
 
@@ -273,7 +274,7 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         a.prof_stats_repeat = int(prof_events[2]) if len(prof_events) > 2 else 1
     _lib.check(lib.sd_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_verify")
     if isinstance(noise, StreamNoise) and sync_noise:
-        noise.advance(int(out.words_used.item()))
+        noise.consumed(used_dev=out.words_used)
     del keep
     return out
 
@@ -345,6 +346,6 @@ def ngram_verify(target_rows: Sequence[torch.Tensor], draft_tokens: Optional[tor
     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
     _lib.check(lib.sd_ngram_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_ngram_verify")
     if isinstance(noise, StreamNoise) and sync_noise:
-        noise.advance(int(out.words_used.item()))
+        noise.consumed(used_dev=out.words_used)
     del keep
     return out

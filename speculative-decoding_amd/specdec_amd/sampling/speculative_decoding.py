@@ -20,7 +20,7 @@ import torch
 from torch.nn import Module
 
 from .. import _lib
-from ..noise import PhiloxNoise, default_noise
+from ..noise import PhiloxNoise, default_noise, noise_session
 from ..ops import proc_spec, sample_rows, verify
 from ..utils.caching import prune_cache
 from ..utils.logits_processor import GreedyProcessor, LogitsProcessor
@@ -66,8 +66,16 @@ def speculative_generate(
     first_target: bool = True,
     debug: bool = False,
 ) -> Tuple[List[int], float]:
-    spec = proc_spec(logits_processor)
     noise = default_noise()
+    with noise_session(noise):   # STREAM: the generator state stays on the device for the loop
+        return _speculative_generate(noise, inputs, drafter, target, gamma, logits_processor, max_gen_len,
+                                     eos_tokens_id, pad_token_id, use_cache, skip_sample_adjustment, first_target,
+                                     debug)
+
+
+def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processor, max_gen_len, eos_tokens_id,
+                          pad_token_id, use_cache, skip_sample_adjustment, first_target, debug):
+    spec = proc_spec(logits_processor)
     dev = target.device
     if torch.device(dev).type != "cuda":
         raise RuntimeError("specdec_amd.speculative_generate runs on the GPU (HIP); the target is on "

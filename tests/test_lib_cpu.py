@@ -51,6 +51,10 @@ int main(void) {
   F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes) F(sd_noise, row_base)
   F(sd_ngram_args, target_rows) F(sd_ngram_args, draft_tokens) F(sd_ngram_args, proc) F(sd_ngram_args, noise)
   F(sd_ngram_args, filler_ids) F(sd_ngram_args, workspace_bytes)
+  printf("sd_mt_state %zu\n", sizeof(sd_mt_state));
+  printf("sd_mt_generate_args %zu\n", sizeof(sd_mt_generate_args));
+  F(sd_mt_state, tau0) F(sd_mt_generate_args, jump_count) F(sd_mt_generate_args, stride_words)
+  F(sd_mt_generate_args, n_words) F(sd_mt_generate_args, workspace_bytes)
   return 0;
 }
 """
@@ -66,7 +70,8 @@ def test_ctypes_layout_matches_c_header():
     got = dict(line.rsplit(" ", 1) for line in out if line)
     for name, cls in [("sd_verify_args", _lib.sd_verify_args), ("sd_sample_args", _lib.sd_sample_args),
                       ("sd_probs_args", _lib.sd_probs_args), ("sd_noise", _lib.sd_noise),
-                      ("sd_ngram_args", _lib.sd_ngram_args), ("sd_ngram_store", _lib.sd_ngram_store)]:
+                      ("sd_ngram_args", _lib.sd_ngram_args), ("sd_ngram_store", _lib.sd_ngram_store),
+                      ("sd_mt_state", _lib.sd_mt_state), ("sd_mt_generate_args", _lib.sd_mt_generate_args)]:
         assert int(got[name]) == C.sizeof(cls), name
     for key, val in got.items():
         if "." in key:
@@ -127,12 +132,28 @@ def test_no_kernel_uses_scratch():
     from specdec_amd import _lib
     if not (os.path.exists(os.path.join(llvm, "clang-offload-bundler")) and os.path.exists(os.path.join(llvm, "llvm-readelf"))):
         pytest.skip("ROCm llvm tools not found")
-    with tempfile.TemporaryDirectory() as d:
-        fb, co = os.path.join(d, "fb.bin"), os.path.join(d, "co.o")
-        subprocess.check_call(["objcopy", "--dump-section", f".hip_fatbin={fb}", _lib.LIB_PATH, os.path.join(d, "x.so")])
-        subprocess.check_call([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", f"--input={fb}", f"--output={co}",
-                               "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"])
-        notes = subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", co]).decode()
+    notes = kernel_notes(_lib.LIB_PATH, llvm)
+    names = re.findall(r"\.name:\s*(\S+)", notes)
+    assert any("k_mt_jump" in n for n in names) and any("k_stats" in n for n in names)
     sizes = re.findall(r"\.private_segment_fixed_size:\s*(\d+)", notes)
     assert len(sizes) > 100
     assert all(int(v) == 0 for v in sizes), sorted(set(sizes))
+
+
+def kernel_notes(lib_path, llvm):
+    """Code-object notes of every gfx950 bundle in the library's .hip_fatbin section (one bundle
+    per HIP translation unit, concatenated by the linker)."""
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    out = []
+    with tempfile.TemporaryDirectory() as d:
+        fb = os.path.join(d, "fb.bin")
+        subprocess.check_call(["objcopy", "--dump-section", f".hip_fatbin={fb}", lib_path, os.path.join(d, "x.so")])
+        data = open(fb, "rb").read()
+        starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+        for i, st in enumerate(starts):
+            part, co = os.path.join(d, f"b{i}.bin"), os.path.join(d, f"co{i}.o")
+            open(part, "wb").write(data[st:starts[i + 1] if i + 1 < len(starts) else len(data)])
+            subprocess.check_call([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", f"--input={part}",
+                                   f"--output={co}", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"])
+            out.append(subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", co]).decode())
+    return "\n".join(out)
