@@ -58,6 +58,7 @@ class _DeviceMT:
         _lib.check(lib.sd_mt19937_state_from_torch(st.data_ptr(), st.numel(), C.byref(host)),
                    "sd_mt19937_state_from_torch")
         raw = np.frombuffer(bytes(host), dtype=np.uint8).copy()
+        self._loaded = raw.tobytes()
         self.state = torch.from_numpy(raw).to(self.device)
         self.words = torch.empty(0, dtype=torch.int32, device=self.device)
         self.ws = torch.empty(0, dtype=torch.uint8, device=self.device)
@@ -88,8 +89,14 @@ class _DeviceMT:
                    "sd_mt19937_commit")
 
     def pull(self, gen: torch.Generator) -> None:
-        """Write the device state back into the torch generator (one device->host copy)."""
-        host = _lib.sd_mt_state.from_buffer_copy(self.state.cpu().numpy().tobytes())
+        """Write the device state back into the torch generator (one device->host copy).  A state
+        that consumed nothing is left as torch holds it: a freshly seeded torch state (left=1,
+        next=0, block not yet twisted) and its converted form (tau0=624) are the same stream but
+        not the same bytes."""
+        raw = self.state.cpu().numpy().tobytes()
+        if raw == self._loaded:
+            return
+        host = _lib.sd_mt_state.from_buffer_copy(raw)
         st = gen.get_state().clone()
         _lib.check(lib.sd_mt19937_state_to_torch(C.byref(host), st.data_ptr(), st.numel()),
                    "sd_mt19937_state_to_torch")
