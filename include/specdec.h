@@ -102,6 +102,9 @@ typedef struct {
 #define SD_ROW_NOISE_OVERRUN  0x80  /* STREAM noise buffer too short                           */
 #define SD_ROW_NUCLEUS_INEXACT 0x100 /* nucleus cut computed where fp32 cumsum rounding could not
                                        be reproduced exactly           */
+#define SD_ROW_EXCHANGE_TIMEOUT 0x200 /* a workgroup's partial never arrived within the bounded
+                                       wait of an in-launch exchange (k_draw_lean); the row's
+                                       outputs are invalid (also flagged SD_ROW_INVALID_DIST)    */
 
 typedef struct {
     /* shape */

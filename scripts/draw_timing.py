@@ -27,7 +27,7 @@ for _ in range(20):
 torch.cuda.synchronize()
 os.environ["SD_TS_PTR"] = str(ts.data_ptr())
 warm = torch.randn(8192, 8192, device=dev)
-phases = ["start", "y_ready", "picked", "arrived", "tail_staged", "tail_picked", "written"]
+phases = ["start", "y_ready", "picked", "arrived", "tail_staged", "tail_picked", "written", "exps_done", "cand_shared"]
 for rep in range(3):
     ts.zero_()
     torch.cuda.synchronize()
@@ -38,6 +38,8 @@ for rep in range(3):
     ops.sample_rows(x, ops.PLAIN_SOFTMAX, noise, row_stats_out=stats)
     torch.cuda.synchronize()
     t = ts.view(-1, 16).cpu().numpy().astype(np.int64)[:8192]
+    if os.environ.get("TS_DUMP"):
+        np.save(os.path.join(ROOT, "gpurun_out", f"draw_ts_rep{rep}.npy"), t)
     blk = t[t[:, 0] > 0]
     t0 = blk[:, 0].min()
     print(f"--- rep {rep}: {len(blk)} workgroups")

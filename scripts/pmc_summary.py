@@ -54,7 +54,7 @@ def main():
     pj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     rec = json.load(open(pj)) if os.path.exists(pj) else {}
     for fam in ("k_draw", "k_stats", "k_sample"):
-        cands = sorted((k for k in acc if k.startswith("sd::" + fam + "<")),
+        cands = sorted((k for k in acc if k.startswith(("sd::" + fam + "<", "sd::" + fam + "_lean<"))),
                        key=lambda k: -max(len(v) for v in acc[k].values()))
         if not cands:
             continue

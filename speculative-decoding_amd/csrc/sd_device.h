@@ -82,6 +82,31 @@ __device__ __forceinline__ void unpack16(const uint4 w, float* out) {
     }
 }
 
+// Split loads: a thread that needs several 16-byte vectors issues them all before it uses any
+// (load_vec's in-range test is a branch, and the compiler waits for each vector before the next
+// branch, so a loop of load_vec calls pays one memory round trip per vector).  ld16_clamped
+// loads the vector at e0, or — past the last whole vector of the row — that last whole vector,
+// so every load is unconditional and in bounds (caller: 16-byte aligned row, vocab >= kVec);
+// finish16 unpacks it and patches a vector that is not wholly inside [0, vocab) with guarded
+// element loads (only a ragged row end takes that second round trip).
+template <int DT>
+__device__ __forceinline__ int64_t last_whole_vec(int vocab) {
+    return ((int64_t)vocab / Elem<DT>::kVec - 1) * Elem<DT>::kVec;
+}
+template <int DT>
+__device__ __forceinline__ uint4 ld16_clamped(const void* row, int64_t e0, int64_t last) {
+    return *reinterpret_cast<const uint4*>(static_cast<const char*>(row) + (e0 < last ? e0 : last) * Elem<DT>::kBytes);
+}
+template <int DT>
+__device__ __forceinline__ void finish16(uint4 w, const void* row, int64_t e0, int vocab, float* out) {
+    constexpr int V = Elem<DT>::kVec;
+    unpack16<DT>(w, out);
+    if (e0 + V > vocab) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) out[k] = (e0 + k < vocab) ? load_one<DT>(row, e0 + k) : 0.f;
+    }
+}
+
 // Load one 16-byte vector (kVec elements) starting at element e0, or the in-range part of it.
 template <int DT>
 __device__ __forceinline__ void load_vec(const void* row, int64_t e0, int vocab, bool aligned, float* out) {

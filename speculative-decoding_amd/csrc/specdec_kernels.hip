@@ -126,6 +126,7 @@ struct Plan {
         if (threadIdx.x == 0 && P.ts) {                                                        \
             P.ts[(size_t)(wg) * 16 + (ph)] = __builtin_amdgcn_s_memrealtime();                 \
             if ((ph) == 4 || (ph) == 10) P.ts[(size_t)(wg) * 16 + 12 + ((ph) == 10)] = __builtin_amdgcn_s_memtime(); \
+            if ((ph) == 1 || (ph) == 2) P.ts[(size_t)(wg) * 16 + 14 + ((ph) == 2)] = __builtin_amdgcn_s_memtime(); \
         }                                                                                      \
     } while (0)
 #else
@@ -1233,9 +1234,18 @@ template <int TDT, int DDT, bool FAST>
 __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, float* w, float* pw = nullptr) {
     constexpr int VEC = PairVec<TDT, DDT>::kVec;
     float xt[VEC], xd[VEC];
-    load_vecn<TDT, VEC>(R.trow, e0, R.V, R.t_al, xt);
-    if (R.resid) {
-        load_vecn<DDT, VEC>(R.drow, e0, R.V, R.d_al, xd);   // dprobs dispatches DDT = F32
+    if (VEC == Elem<TDT>::kVec && VEC == Elem<DDT>::kVec && R.t_al && (!R.resid || R.d_al) && R.V >= VEC) {
+        // both rows' vectors in flight together (ld16_clamped), one round trip
+        const uint4 wt = ld16_clamped<TDT>(R.trow, e0, last_whole_vec<TDT>(R.V));
+        uint4 wd = make_uint4(0u, 0u, 0u, 0u);
+        if (R.resid) wd = ld16_clamped<DDT>(R.drow, e0, last_whole_vec<DDT>(R.V));
+        finish16<TDT>(wt, R.trow, e0, R.V, xt);
+        if (R.resid) finish16<DDT>(wd, R.drow, e0, R.V, xd);
+    } else {
+        load_vecn<TDT, VEC>(R.trow, e0, R.V, R.t_al, xt);
+        if (R.resid) {
+            load_vecn<DDT, VEC>(R.drow, e0, R.V, R.d_al, xd);   // dprobs dispatches DDT = F32
+        }
     }
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
@@ -1278,16 +1288,16 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
 // of the fp64 running sum in (thread, k) order holds u * total.  Every element's interval has its
 // exact fp32 weight as width.  Returns the position tid * EPT + k (uniform), -1 without positive
 // weight; total: the chunk's fp64 Σ weight, ptotal: the block sum of pextra (fixed order).
+// chunk_pick_tot: the same with the thread's total given (k_draw's lean path sums its weights in
+// fp32: the walk's fp64 intervals then tile the thread's interval up to that rounding, ~EPT ulp).
 template <int EPT>
-__device__ __forceinline__ int chunk_pick(const float* wv, double u, float pextra, double& total, float& ptotal) {
+__device__ __forceinline__ int chunk_pick_tot(const float* wv, double tot, double u, float pextra, double& total,
+                                              float& ptotal) {
     constexpr int NW = kThreads / kWave;
     __shared__ double s_wtot[NW];
     __shared__ float s_ptot[NW];
     __shared__ int s_pos[NW], s_lastp[NW];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    double tot = 0.0;
-#pragma unroll
-    for (int k = 0; k < EPT; ++k) tot += (double)wv[k];
     // exclusive fp64 prefix of the thread totals in thread order: DPP scan, wave offsets via LDS
     const double wincl = wave_incl_scan_d(tot);
     double excl = dpp_d<0x138, 0xF, true>(0.0, wincl);   // wave_shr:1 -> the previous lane's inclusive
@@ -1346,6 +1356,13 @@ __device__ __forceinline__ int chunk_pick(const float* wv, double u, float pextr
     }
     // rounding can leave t at/after the running total's end: the last positive element
     return pos == INT_MAX ? lp : pos;
+}
+template <int EPT>
+__device__ __forceinline__ int chunk_pick(const float* wv, double u, float pextra, double& total, float& ptotal) {
+    double tot = 0.0;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) tot += (double)wv[k];
+    return chunk_pick_tot<EPT>(wv, tot, u, pextra, total, ptotal);
 }
 
 // vocabulary index of chunk_pick's position in the chunk starting at base
@@ -1669,21 +1686,94 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
     const RowKeep kp = (!FAST && P.t_keep) ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const int64_t base = (int64_t)c * NST * STEP;
-    // both uniforms up front (ALU only), overlapping the loads: the span's in-chunk draw and, in
-    // case this workgroup is the row's last arrival, the tail's chunk pick
-    const double u_c = cdf_uniform(P.noise, (uint32_t)r, 1u + (uint32_t)c);
-    const double u_row = cdf_uniform(P.noise, (uint32_t)r);
+    // The Philox uniforms run on the scalar unit, which every wave of the CU shares: computed by
+    // each wave ahead of its loads (as the compiler scheduled them) they held back the launch's
+    // load issue by ~0.7 us.  So: loads first, the span's in-chunk uniform by wave 0 alone (into
+    // LDS; the span-max barrier publishes it), the tail's chunk-pick uniform by the tail's wave 1.
+    __shared__ double s_u;
+    double u_c;
     float y[EPT];
+    float wv[EPT];
+    double T;
+    float PT;
+    int pos;
+    float m;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // lean path (T = 1, no processor, 16-bit rows, aligned, the span wholly inside the row — every
+    // span of a row but its ragged last one): no per-element bounds, NaN or keep tests; the
+    // compute phase is VALU-bound (every workgroup of the launch reaches it at once), so each
+    // element costs an unpack, a max3 third, a subtract, a multiply, an exp and an fp32 add.
+    // A NaN / +inf anywhere makes the fp32 total NaN, which flags the row as the general path does.
+    constexpr bool kLeanOk = FAST && DT != SD_F32;
+    if (kLeanOk && al && base + (int64_t)NST * STEP <= P.V) {
+        uint4 raw[NST];
 #pragma unroll
-    for (int v = 0; v < NST; ++v) {
-        const int64_t e0 = base + (int64_t)v * STEP + threadIdx.x * VEC;
-        float x[VEC];
-        load_vec<DT>(row, e0, P.V, al, x);
+        for (int v = 0; v < NST; ++v)
+            raw[v] = *reinterpret_cast<const uint4*>(static_cast<const char*>(row) + (base + (int64_t)v * STEP + threadIdx.x * VEC) * 2);
+        if (w == 0) {
+            const double u = cdf_uniform(P.noise, (uint32_t)r, 1u + (uint32_t)c);
+            if (lane == 0) s_u = u;
+        }
+#pragma unroll
+        for (int v = 0; v < NST; ++v) unpack16<DT>(raw[v], y + v * VEC);
+        float mv = y[0];
+#pragma unroll
+        for (int k = 1; k + 1 < EPT; k += 2) mv = fmaxf(mv, fmaxf(y[k], y[k + 1]));
+        if constexpr (EPT % 2 == 0) mv = fmaxf(mv, y[EPT - 1]);
+        mv = wave_max(mv);
+        if (lane == 0) lm[w] = mv;
+        __syncthreads();
+        m = lm[0];
+#pragma unroll
+        for (int k = 1; k < kThreads / kWave; ++k) m = fmaxf(m, lm[k]);
+        u_c = s_u;
+        SD_TS(wg_id, 1);
+        float t32 = 0.f;
+        if (m > -INFINITY) {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                wv[k] = __builtin_amdgcn_exp2f((y[k] - m) * kLog2e);
+                t32 += wv[k];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) wv[k] = 0.f;
+        }
+        SD_TS(wg_id, 7);
+        pos = chunk_pick_tot<EPT>(wv, (double)t32, u_c, 0.f, T, PT);
+        if (T != T) PT = 1.f;   // NaN / +inf in the span: the general path's flag
+    } else {
+    auto take = [&](int v, int64_t e0, const float* x) {
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const float yk = FAST ? x[k] : process_value<DT>(x[k], e0 + k, P.tT, P.t_keep, kp);
             y[v * VEC + k] = e0 + k < P.V ? yk : -INFINITY;
         }
+    };
+    if (al && P.V >= VEC) {   // every stage's vector in flight at once (ld16_clamped)
+        const int64_t last = last_whole_vec<DT>(P.V);
+        uint4 raw[NST];
+#pragma unroll
+        for (int v = 0; v < NST; ++v) raw[v] = ld16_clamped<DT>(row, base + (int64_t)v * STEP + threadIdx.x * VEC, last);
+#pragma unroll
+        for (int v = 0; v < NST; ++v) {
+            const int64_t e0 = base + (int64_t)v * STEP + threadIdx.x * VEC;
+            float x[VEC];
+            finish16<DT>(raw[v], row, e0, P.V, x);
+            take(v, e0, x);
+        }
+    } else {
+#pragma unroll
+        for (int v = 0; v < NST; ++v) {
+            const int64_t e0 = base + (int64_t)v * STEP + threadIdx.x * VEC;
+            float x[VEC];
+            load_vec<DT>(row, e0, P.V, al, x);
+            take(v, e0, x);
+        }
+    }
+    if (w == 0) {
+        const double u = cdf_uniform(P.noise, (uint32_t)r, 1u + (uint32_t)c);
+        if (lane == 0) s_u = u;
     }
     // span max (NaN sticks: fmaxf drops it, so track it apart)
     float mv = -INFINITY;
@@ -1694,19 +1784,17 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
         nan |= y[k] != y[k];
     }
     mv = wave_max(mv);
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (lane == 0) lm[w] = mv;
     __syncthreads();
-    float m = lm[0];
+    m = lm[0];
 #pragma unroll
     for (int k = 1; k < kThreads / kWave; ++k) m = fmaxf(m, lm[k]);
+    u_c = s_u;
     SD_TS(wg_id, 1);
-    float wv[EPT];
 #pragma unroll
     for (int k = 0; k < EPT; ++k) wv[k] = m > -INFINITY ? __builtin_amdgcn_exp2f((y[k] - m) * kLog2e) : 0.f;
-    double T;
-    float PT;
-    const int pos = chunk_pick<EPT>(wv, u_c, nan ? 1.f : 0.f, T, PT);
+    pos = chunk_pick<EPT>(wv, u_c, nan ? 1.f : 0.f, T, PT);
+    }
     SD_TS(wg_id, 2);
     // the candidate's processed value, from the thread that holds it
     __shared__ float s_ycand;
@@ -1718,6 +1806,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
         s_ycand = yc;
     }
     __syncthreads();
+    SD_TS(wg_id, 8);
     // partial (m_c, S_c | j_c, y_{j_c}) as one 16-byte write-through store into the span's slot
     float2* slot = reinterpret_cast<float2*>(reinterpret_cast<float4*>(P.rpart) + (int64_t)r * P.n_chunks + c);
     if (threadIdx.x == 0) {
@@ -1750,6 +1839,10 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     }
     __syncthreads();
     SD_TS(wg_id, 4);
+    if (w == 1) {   // the chunk-pick uniform, beside wave 0's combine
+        const double u = cdf_uniform(P.noise, (uint32_t)r);
+        if (lane == 0) s_u = u;
+    }
     if (threadIdx.x < kWave) {
         float M = -INFINITY;
         for (int k = lane; k < P.n_chunks; k += kWave) M = fmaxf(M, l_w[k]);
@@ -1765,7 +1858,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     }
     __syncthreads();
     const float2 ms = s_ms;
-    const int cp = pick_chunk(P, u_row, l_w);
+    const int cp = pick_chunk(P, s_u, l_w);
     SD_TS(wg_id, 5);
     if (threadIdx.x == 0) {
         int32_t st = SD_ROW_DONE;
@@ -1782,6 +1875,282 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     SD_TS(wg_id, 6);
 }
 static_assert(sizeof(ResPart) >= sizeof(float4), "k_draw keeps a 16-byte partial per span in the ResPart region");
+static_assert(2 * sizeof(ResPart) >= 8 * sizeof(float4), "k_draw_lean's line-padded rows fit the (nc + 1) ResParts per row");
+
+// ------------------------------------------------------------------ k_draw_lean
+// The bench's draw (and the drop-in loops' common case): T = 1, no processor, 16-bit rows,
+// 16-byte aligned.  Same draw and outputs as k_draw, restructured for the latency chain that
+// bounds a 8 MB launch (scripts/microbench/draw_shapes.hip: a bare span pass over the same rows
+// takes 3.5 us):
+//   * a compact kernel-argument block (one scalar-load batch, no hidden-argument division);
+//   * spans of NST x 2048 elements, every vector in flight at once, no per-element tests except
+//     in a row's ragged last span;
+//   * the thread holding the span's candidate stores the partial itself (no candidate barrier)
+//     and its wave alone continues: arrival, and — for the row's last arrival — the whole tail
+//     in that one wave (64 lanes stage up to 64 partials per pass; wave reductions and a DPP
+//     scan; no barrier).
+struct DrawLean {
+    const char* rows;
+    int64_t stride_bytes;
+    float4* part;
+    uint32_t* cnt;
+    int64_t* next_token;
+    int64_t nt_stride;
+    float* token_prob;
+    float2* row_stats;
+    int32_t* row_status;
+    int64_t* words_used;
+    sd_noise noise;
+    int32_t V, n_span;
+    int32_t pstride;   // float4 partials per row: n_span rounded up to whole 128-B lines
+    int32_t poll;      // 1: the row's last span polls tagged partials (no arrival counter)
+};
+
+// Poll-mode record tag: the row's epoch (counter set 2, advanced by the row's consumer after every
+// draw) hashed with the row, the span and the span count.  Every row advances its epoch in step,
+// and other shapes place other rows' records at these addresses, so the epoch alone would match
+// a record another row left here; bytes from other kernels match only by a 2^-32 accident.
+__device__ __forceinline__ uint32_t draw_tag(uint32_t epoch, int r, int c, int n_span) {
+    uint32_t h = epoch * 0x9E3779B1u + (uint32_t)r * 0x85EBCA77u + (uint32_t)c * 0xC2B2AE3Du + (uint32_t)n_span * 0x27D4EB2Fu;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;   // murmur3 fmix32
+    return h | 1u;   // never 0 (zero-filled workspace)
+}
+
+template <int DT, int NST>
+__global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
+    constexpr int VEC = 8, STEP = kThreads * VEC, EPT = NST * VEC, NW = kThreads / kWave;
+    const int c = blockIdx.x, r = blockIdx.y;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const char* row = A.rows + (int64_t)r * A.stride_bytes;
+    const int64_t base = (int64_t)c * NST * STEP;
+    float y[EPT];
+    if (base + (int64_t)NST * STEP <= A.V) {
+        uint4 raw[NST];
+#pragma unroll
+        for (int v = 0; v < NST; ++v)
+            raw[v] = *reinterpret_cast<const uint4*>(row + (base + (int64_t)v * STEP + threadIdx.x * VEC) * 2);
+#pragma unroll
+        for (int v = 0; v < NST; ++v) unpack16<DT>(raw[v], y + v * VEC);
+    } else {   // the row's ragged last span
+        const int64_t last = last_whole_vec<DT>(A.V);
+        uint4 raw[NST];
+#pragma unroll
+        for (int v = 0; v < NST; ++v) raw[v] = ld16_clamped<DT>(row, base + (int64_t)v * STEP + threadIdx.x * VEC, last);
+#pragma unroll
+        for (int v = 0; v < NST; ++v) {
+            const int64_t e0 = base + (int64_t)v * STEP + threadIdx.x * VEC;
+            finish16<DT>(raw[v], row, e0, A.V, y + v * VEC);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) y[v * VEC + k] = e0 + k < A.V ? y[v * VEC + k] : -INFINITY;
+        }
+    }
+    __shared__ float l_m[NW], l_s[NW];
+    __shared__ double l_u;
+    __shared__ int32_t l_j;
+    __shared__ float l_y;
+    uint32_t epoch = 0;   // poll mode: this launch's epoch of row r (read by wave 0, beside the loads)
+    if (w == 0) {   // the span's in-chunk uniform: one wave's scalar unit, while the loads fly
+        if (A.poll) epoch = __hip_atomic_load(seq_counter(A.cnt, 2, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double u = cdf_uniform(A.noise, (uint32_t)r, 1u + (uint32_t)c);
+        if (lane == 0) { l_u = u; l_j = -1; l_y = -INFINITY; }
+    }
+    // per-wave max and weights: no barrier before the exps
+    float mv = y[0];
+#pragma unroll
+    for (int k = 1; k < EPT; ++k) mv = fmaxf(mv, y[k]);
+    const float mw = wave_max(mv);
+    float wv[EPT];
+    float tl = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        wv[k] = mw > -INFINITY ? __builtin_amdgcn_exp2f((y[k] - mw) * kLog2e) : 0.f;
+        tl += wv[k];
+    }
+    const float incl = wave_incl_scan(tl);             // lane order, relative to mw
+    const float prev = dpp_f<0x138, 0xF, true>(0.f, incl);   // wave_shr:1 -> the previous lane's incl
+    if (lane == 63) { l_m[w] = mw; l_s[w] = incl; }
+    __syncthreads();
+    // every thread: span max, wave weights, offsets and total in one fixed order (uniform)
+    float m = l_m[0];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) m = fmaxf(m, l_m[k]);
+    float off = 0.f, my_off = 0.f, my_sc = 0.f, my_W = 0.f;
+    int lastw = -1;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const float sc = l_m[k] > -INFINITY ? __builtin_amdgcn_exp2f((l_m[k] - m) * kLog2e) : 0.f;
+        const float Wk = l_s[k] * sc;
+        if (k == w) { my_off = off; my_sc = sc; my_W = Wk; }
+        if (Wk > 0.f) lastw = k;
+        off += Wk;
+    }
+    const float T = off;
+    const float t = (float)(l_u * (double)T);
+    // the claiming wave (rounding past the end: the last wave with weight)
+    const bool claim = my_W > 0.f && ((t >= my_off && t < my_off + my_W) || (w == lastw && t >= my_off + my_W));
+    if (claim) {
+        const float a = fmaf(incl, my_sc, my_off), a0 = lane == 0 ? my_off : fmaf(prev, my_sc, my_off);
+        const uint64_t hit = __ballot(a > t && tl > 0.f), posm = __ballot(tl > 0.f);
+        const int hl = hit ? __builtin_ctzll(hit) : (posm ? 63 - __builtin_clzll(posm) : -1);
+        if (lane == hl) {
+            float run = a0;
+            int kk = -1, lastk = -1;
+#pragma unroll
+            for (int k = 0; k < EPT; ++k) {
+                run = fmaf(wv[k], my_sc, run);
+                if (wv[k] > 0.f) {
+                    lastk = k;
+                    if (kk < 0 && run > t) kk = k;
+                }
+            }
+            if (kk < 0) kk = lastk;
+            if (kk >= 0) {
+                const int v = kk / VEC;
+                float yk = y[0];
+#pragma unroll
+                for (int k = 1; k < EPT; ++k) yk = k == kk ? y[k] : yk;
+                l_j = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + (kk - v * VEC));
+                l_y = yk;
+            }
+        }
+    }
+    __syncthreads();
+    if (w != 0) return;
+    const bool bad = T != T;   // NaN / +inf in the span: S_c NaN flags the row
+    const float m_pub = bad && !(m > -INFINITY) ? 0.f : m, s_pub = bad ? NAN : T;
+    const int32_t j_pub = l_j;
+    const float y_pub = l_y;
+    float4* part_row = A.part + (int64_t)r * A.pstride;
+    int32_t xstat = 0;
+    if (A.poll) {
+        // Poll mode: every span but the row's last publishes one tagged 16-byte record
+        // {m_c, S_c, (j_c - base + 1) | raw y << 16, tag} (write-through) and is done; the last
+        // span's wave 0 polls the records until every tag is this launch's (bounded), then runs
+        // the tail and advances the row's epoch.  No counter, no write-ack wait on the path.
+        const uint32_t tag = draw_tag(epoch, r, c, A.n_span);
+        if (c != A.n_span - 1) {
+            if (threadIdx.x == 0) {
+                const uint32_t yraw = DT == SD_BF16 ? (__float_as_uint(y_pub) >> 16)
+                                                    : (uint32_t)__half_as_ushort(__float2half_rn(y_pub));
+                const uint32_t off = j_pub >= 0 ? (uint32_t)(j_pub - base) + 1u : 0u;   // <= NST * 2048
+                st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), off | (yraw << 16), tag));
+            }
+            return;
+        }
+    } else {
+        // counter mode (many rows: more consumers than resident workgroups could spin): thread 0
+        // publishes {m_c, S_c, j_c, y_{j_c}} and arrives; the last arrival runs the tail
+        uint32_t last = 0;
+        if (threadIdx.x == 0) {
+            st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), (uint32_t)j_pub,
+                                              __float_as_uint(y_pub)));
+            last = arrive_last(seq_counter(A.cnt, 0, r), (uint32_t)A.n_span) ? 1u : 0u;
+        }
+        if (!__builtin_amdgcn_readlane(last, 0)) return;
+    }
+
+    // ---- tail (one wave): every span's partial, M, S, the span pick, the outputs
+    const float2* pr = reinterpret_cast<const float2*>(A.part + (int64_t)r * A.pstride);
+    float M = -INFINITY;
+    float mk[2], sk[2], yk[2];
+    int32_t jk[2];
+    const int npass = (A.n_span + kWave - 1) / kWave;   // <= 2 (host: n_span <= 128)
+    const double u_row = cdf_uniform(A.noise, (uint32_t)r);   // scalar unit, before the wait
+    if (A.poll) {
+        // every other span's record, re-read until its tag is this launch's; this span's own from
+        // registers (the lane that would hold it)
+        bool have[2];
+        uint4 rec[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = q * kWave + lane;
+            have[q] = !(q < npass && k < A.n_span) || k == c;
+            rec[q] = make_uint4(0u, 0u, 0u, 0u);
+        }
+        for (int spin = 0;; ++spin) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                if (!have[q]) {
+                    rec[q] = ld_coh16(pr + 2 * (q * kWave + lane));
+                    have[q] = rec[q].w == draw_tag(epoch, r, q * kWave + lane, A.n_span);
+                }
+            }
+            if (__all(have[0] && have[1])) break;
+            if (spin >= (1 << 16)) {   // bounded: ~tens of ms; the row is flagged, never a hang
+                xstat = SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = q * kWave + lane;
+            mk[q] = -INFINITY; sk[q] = 0.f; yk[q] = -INFINITY; jk[q] = -1;
+            if (k == c) {
+                mk[q] = m_pub; sk[q] = s_pub; jk[q] = j_pub; yk[q] = y_pub;
+            } else if (q < npass && k < A.n_span && have[q]) {
+                mk[q] = __uint_as_float(rec[q].x); sk[q] = __uint_as_float(rec[q].y);
+                const uint32_t off = rec[q].z & 0xffffu, yraw = rec[q].z >> 16;
+                jk[q] = off ? (int32_t)((int64_t)k * NST * STEP + off - 1) : -1;
+                yk[q] = DT == SD_BF16 ? __uint_as_float(yraw << 16) : __half2float(__ushort_as_half((unsigned short)yraw));
+            }
+            M = fmaxf(M, mk[q]);
+        }
+    } else {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int k = q * kWave + lane;
+        mk[q] = -INFINITY; sk[q] = 0.f; yk[q] = -INFINITY; jk[q] = -1;
+        if (q < npass && k < A.n_span) {
+            const uint4 v = ld_coh16(pr + 2 * k);
+            mk[q] = __uint_as_float(v.x); sk[q] = __uint_as_float(v.y);
+            jk[q] = (int32_t)v.z; yk[q] = __uint_as_float(v.w);
+        }
+        M = fmaxf(M, mk[q]);
+    }
+    }
+    M = wave_max(M);
+    float wk[2], S = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        wk[q] = mk[q] > -INFINITY || sk[q] != sk[q] ? sk[q] * sd_exp(mk[q] - M) : 0.f;
+        S += wk[q];
+    }
+    S = wave_sum(S);
+    // span pick: first span whose fp64 running total (span order) exceeds u * Σ
+    double base_d = 0.0, tot = 0.0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) tot += lane_d(wave_incl_scan_d((double)wk[q]), 63);
+    const double tt = u_row * tot;
+    int pick = -1, lastpos = -1;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const double incl2 = base_d + wave_incl_scan_d((double)wk[q]);
+        const uint64_t hit = __ballot(incl2 > tt && wk[q] > 0.f), posm = __ballot(wk[q] > 0.f);
+        if (pick < 0 && hit) pick = q * kWave + __builtin_ctzll(hit);
+        if (posm) lastpos = q * kWave + 63 - __builtin_clzll(posm);
+        base_d = lane_d(incl2, 63);
+    }
+    if (pick < 0) pick = lastpos;   // rounding left t at / after the total: the last positive span
+    int32_t x = -1;
+    float yx = -INFINITY;
+    if (pick >= 0) {
+        const int q = pick / kWave, src = pick & 63;
+        x = __builtin_amdgcn_readlane(q == 0 ? jk[0] : jk[1], src);
+        yx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(q == 0 ? yk[0] : yk[1]), src));
+    }
+    if (lane == 0) {
+        int32_t st = SD_ROW_DONE | xstat;
+        if (!(S > 0.f) || S != S || S == INFINITY) st |= SD_ROW_INVALID_DIST;   // torch raises
+        if (x < 0) st |= SD_ROW_INVALID_DIST;
+        if (A.poll) __hip_atomic_store(seq_counter(A.cnt, 2, r), epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        A.next_token[r * A.nt_stride] = x;
+        if (A.token_prob) A.token_prob[r] = x >= 0 ? prob_exact<DT>(yx, M, S, 1.0f / S) : NAN;
+        if (A.row_stats) A.row_stats[r] = make_float2(M, S);
+        if (A.row_status) A.row_status[r] = st;
+        if (r == 0 && A.words_used) *A.words_used = 0;
+    }
+}
 
 // ------------------------------------------------------------------ sd_probs kernel
 template <int DT, int EPT>
@@ -1853,14 +2222,15 @@ int max_chunks(int vocab) { return (vocab + kThreads * kEptSmall - 1) / (kThread
 
 void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     const int nc = max_chunks(vocab);
-    P.cnt = c.take<uint32_t>(2 * (size_t)kCntMax * kCntStride);   // first, at a fixed offset (see kCntMax)
+    P.cnt = c.take<uint32_t>(3 * (size_t)kCntMax * kCntStride);   // first, at a fixed offset (see kCntMax)
     P.part = c.take<float2>((size_t)rows_total * nc);
     P.rowstat = c.take<float2>(rows_total);
     P.keep = c.take<RowKeep>(rows_total);
     P.rp = c.take<float>((size_t)B * gamma);
     P.rq = c.take<float>((size_t)B * gamma);
     P.dec = c.take<Decision>(B);
-    P.rpart = c.take<ResPart>((size_t)(B > rows_total ? B : rows_total) * nc);
+    // + 1 per row: room for 16-byte records padded to whole 128-B lines per row (k_draw_lean)
+    P.rpart = c.take<ResPart>((size_t)(B > rows_total ? B : rows_total) * (nc + 1));
     P.keep_hist = c.take<int32_t>((size_t)rows_total * kThreshScratchInts);
     P.thr_part = c.take<uint32_t>((size_t)rows_total * kThrMaxSlices);
     P.thr_tail = c.take<float>((size_t)rows_total * kThrMaxSlices);
@@ -2038,7 +2408,52 @@ int32_t launch_draw_dt(const sd::Plan& P, int nst, void* stream) {
     return SD_OK;
 }
 
+// k_draw_lean's cases: T = 1, no processor, 16-bit rows, every row 16-byte aligned, <= 128 spans
+template <int DT, int NST>
+int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
+    DrawLean A{};
+    A.rows = static_cast<const char*>(P.trow[0]);
+    A.stride_bytes = P.tstride * 2;
+    A.part = reinterpret_cast<float4*>(P.rpart);
+    A.cnt = P.cnt;
+    A.next_token = P.next_token; A.nt_stride = P.next_token_stride;
+    A.token_prob = P.token_prob; A.row_stats = P.row_stats; A.row_status = P.row_status; A.words_used = P.words_used;
+    A.noise = P.noise;
+    A.V = P.V;
+    A.n_span = (int32_t)((P.V + NST * kThreads * 8 - 1) / (NST * kThreads * 8));
+    A.pstride = (A.n_span + 7) & ~7;
+    // poll mode needs every row's consumer resident while it waits: at most half the workgroups
+    // the device holds at once (occupancy x CUs, queried once per device) are consumers
+    static int cap[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (cap[dev] == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_draw_lean<DT, NST>, kThreads, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = cus = 0;
+        cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
+    }
+    static const bool no_poll = getenv("SD_DRAW_NO_POLL") != nullptr;   // A/B switch: counter mode only
+    A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && !no_poll;
+    SD_LAUNCH((k_draw_lean<DT, NST>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
+    return SD_OK;
+}
+
 int32_t launch_draw(sd::Plan& P, void* stream) {
+    {
+        const bool fast = P.tT == 1.0f && !P.t_keep && P.tdt != SD_F32;
+        const bool al = (reinterpret_cast<uintptr_t>(P.trow[0]) & 15) == 0 && (P.tstride * 2) % 16 == 0;
+        // A/B switches, read once: SD_DRAW_LEAN_STAGES=2 (4096-element spans), SD_DRAW_NO_LEAN (k_draw only)
+        static const int nst_env = getenv("SD_DRAW_LEAN_STAGES") ? atoi(getenv("SD_DRAW_LEAN_STAGES")) : 1;
+        static const bool no_lean = getenv("SD_DRAW_NO_LEAN") != nullptr;
+        const int nst = nst_env == 2 ? 2 : 1;
+        const int64_t span = (int64_t)nst * kThreads * 8;
+        if (fast && al && P.V >= 8 && (P.V + span - 1) / span <= 128 && !no_lean) {
+            if (P.tdt == SD_BF16) return nst == 2 ? launch_draw_lean_t<SD_BF16, 2>(P, stream) : launch_draw_lean_t<SD_BF16, 1>(P, stream);
+            return nst == 2 ? launch_draw_lean_t<SD_F16, 2>(P, stream) : launch_draw_lean_t<SD_F16, 1>(P, stream);
+        }
+    }
     // spans of NST stages (2048 elements each): 2 once the grid passes ~1024 workgroups
     // (measured at 32 rows of 128256 bf16: NST 1 9.0 us, 2 8.5, 4 10.6 — its registers spill)
     const int64_t stage = kThreads * 8;
@@ -2051,6 +2466,7 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
     P.n_chunks = (int32_t)((P.V + P.chunk - 1) / P.chunk);
     P.rn_chunks = P.n_chunks;   // pick_chunk's count
     P.xcd_affine = P.B % 8 == 0;
+    if (getenv("SD_DRAW_NO_AFFINE")) P.xcd_affine = false;
     if (P.tdt == SD_BF16) return launch_draw_dt<SD_BF16>(P, nst, stream);
     if (P.tdt == SD_F32) return launch_draw_dt<SD_F32>(P, nst, stream);
     return launch_draw_dt<SD_F16>(P, nst, stream);

@@ -27,6 +27,7 @@ SD_ROW_FALLBACK_P = 0x20
 SD_ROW_INVALID_DIST = 0x40
 SD_ROW_NOISE_OVERRUN = 0x80
 SD_ROW_NUCLEUS_INEXACT = 0x100
+SD_ROW_EXCHANGE_TIMEOUT = 0x200
 
 # SPECDEC_LIB selects another in-tree build of the same ABI (e.g. the phase-timing variant)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("SPECDEC_LIB", "libspecdec.so"))

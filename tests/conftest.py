@@ -22,3 +22,15 @@ def pytest_collection_modifyitems(config, items):
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    try:
+        import parity_stats
+    except ImportError:
+        return
+    lines = parity_stats.summary_lines()
+    if lines:
+        terminalreporter.section("parity counts")
+        for ln in lines:
+            terminalreporter.write_line(ln)

@@ -15,6 +15,7 @@ import pytest
 import torch
 
 from oracle import specdec_ref as ref
+from parity_stats import DRAW_CLOSE_CALLS
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -75,6 +76,7 @@ def processed_values(row, proc):
 @pytest.mark.parametrize("label,proc,V,dtype", [
     ("multi_t1_v64", ref.Processor("multinomial", 1.0), 64, torch.bfloat16),
     ("multi_t1_v8192", ref.Processor("multinomial", 1.0), 8192, torch.bfloat16),
+    ("multi_t1_v128256", ref.Processor("multinomial", 1.0), 128256, torch.bfloat16),   # the bench's rows
     ("multi_t07_v50257_f32", ref.Processor("multinomial", 0.7), 50257, torch.float32),
     ("topk50_v8192", ref.Processor("topk", 0.8, 50), 8192, torch.bfloat16),
     ("nucleus09_v8192", ref.Processor("nucleus", 1.0, 0, 0.9), 8192, torch.bfloat16),
@@ -212,6 +214,19 @@ def test_verify_with_draw_stats(sd, rule):
     assert int((na != nb).sum()) <= 1
     same = na == nb
     assert int((a.next_token.cpu()[same] != b.next_token.cpu()[same]).sum()) <= 1
+    # a row whose decision differs must be a close call: at its first differing draft the accept
+    # uniform sits within fp32 rounding of the exact p/q (the two calls differ only in how the
+    # drafter's Σexp was summed)
+    pp = ref.process(tl[:, :g].cpu(), proc, exact=True).double()
+    qq = ref.process(dl.cpu(), proc, exact=True).double()
+    ih = ids.cpu()
+    for s in (~same).nonzero().flatten().tolist():
+        i = min(int(na[s]), int(nb[s]))
+        p_i, q_i = float(pp[s, i, ih[s, i]]), float(qq[s, i, ih[s, i]])
+        ratio = min(1.0, p_i / q_i) if q_i > 0 else 1.0
+        u = float(ph.accept_uniform(11, off, s, i))   # both rules test the same uniform against p/q
+        assert abs(u - ratio) <= 1e-5 * ratio + 1e-7, (s, i, u, ratio)
+        DRAW_CLOSE_CALLS.append(f"{rule} row={s} draft={i} p/q={ratio:.9g} u={u:.9g}")
     assert ((a.row_status.cpu() & sd.lib.SD_ROW_DONE) != 0).all()
     if rule == "engine":   # host walk on the exact p / q
         pt = ref.softmax(tl[:, :g].cpu(), True).float()

@@ -102,7 +102,7 @@ SPEC_GRID = [
 ]
 
 
-DIVERGENCES = []
+from parity_stats import DIVERGENCES, NUCLEUS_ROWS, TIE_DIVERGENCES  # noqa: E402
 
 
 def run_spec_oracle(tl, dl, ids, proc, gen, stops, skip=False, exact=False):
@@ -136,7 +136,6 @@ def _ints(w):
     return (w["n"], w["stop"]) + ((w["x"], w["kd"], w["kt"]) if w["stop"] < 0 else ())
 
 
-TIE_DIVERGENCES = []
 
 
 def oracle_variants(proc):
@@ -177,6 +176,11 @@ def check_spec(sd, tl, dl, ids, proc, seed, stops=(), skip=False):
         match = [label for label, res, _ in variants if _ints(res[b]) == got]
         assert match, (b, got, [(label, res[b]) for label, res, _ in variants], hex(st[b]))
         note_divergence(match[0], f"spec seed={seed} row={b}")
+        if proc.kind in ("nucleus", "topknucleus"):
+            NUCLEUS_ROWS["checked"] += 1
+            if st[b] & sd.lib.SD_ROW_NUCLEUS_INEXACT:   # held to the same integer match, and counted
+                NUCLEUS_ROWS["inexact"] += 1
+                NUCLEUS_ROWS["inexact=" + match[0]] += 1
         # mass vs the exact-arithmetic oracle with the kernel's tie rule (lowest index first)
         ex_label = "exact-stable-ties" if proc.kind in ("nucleus", "topknucleus") else "exact"
         wx = dict((label, res) for label, res, _ in variants)[ex_label][b]
@@ -192,9 +196,12 @@ def check_spec(sd, tl, dl, ids, proc, seed, stops=(), skip=False):
 def test_spec_verify_matches_oracle(sd, B, gamma, V, dtype, kind, seed):
     proc = KINDS[kind]
     tl, dl, ids = draft_case(B, gamma, V, dtype, seed, proc)
+    before = NUCLEUS_ROWS["inexact"]
     st = check_spec(sd, tl, dl, ids, proc, seed)
     if proc.kind in ("nucleus", "topknucleus"):
-        assert all(not (s & sd.lib.SD_ROW_NUCLEUS_INEXACT) or True for s in st)
+        # every row (INEXACT or not) equalled an oracle inside check_spec; the flag count is exact
+        flagged = sum(1 for s in st if s & sd.lib.SD_ROW_NUCLEUS_INEXACT)
+        assert NUCLEUS_ROWS["inexact"] - before == flagged
 
 
 def test_spec_verify_full_accept_bonus(sd):
@@ -469,6 +476,7 @@ def test_divergence_budget():
     nucleus tie-order divergences are reported (torch's unstable sort order is implementation-defined)."""
     print(f"[parity] torch-CPU rounding divergences: {len(DIVERGENCES)} {DIVERGENCES}")
     print(f"[parity] nucleus tie-order divergences: {len(TIE_DIVERGENCES)} {TIE_DIVERGENCES}")
+    print(f"[parity] nucleus rows: {dict(NUCLEUS_ROWS)}")
     assert len(DIVERGENCES) <= 6
 
 

@@ -239,7 +239,7 @@ def _collect(sd, calls, run):
     return np.concatenate(xs)
 
 
-@pytest.mark.parametrize("V,n_hot", [(64, 0), (8192, 40)])
+@pytest.mark.parametrize("V,n_hot", [(64, 0), (8192, 40), (128256, 60)])
 def test_perf_residual_distribution(sd, V, n_hot):
     """SPEC reject at slot 0: the token must follow (p0 - q0)+ / Σ — across sampling chunks too."""
     proc = ref.Processor("multinomial", 1.0)
