@@ -67,9 +67,11 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def graph_steps(step, steps, per_graph):
+def graph_steps(step, steps, per_graph, noise=None, calls_per_step=0):
     """Capture `per_graph` steps in one hipGraph, replay steps // per_graph times (untimed warm replay
-    first).  Returns (graph, outputs of the captured steps, replays)."""
+    first).  Returns (graph, outputs of the captured steps, replays).  With a PhiloxNoise that has
+    a device counter base, the graph ends by moving it past the captured calls, so every replay
+    draws fresh noise (the outputs are those of the last replay)."""
     G = max(1, min(per_graph, steps))
     while steps % G:
         G -= 1
@@ -78,6 +80,8 @@ def graph_steps(step, steps, per_graph):
     with torch.cuda.graph(graph):
         for _ in range(G):
             outs.append(step())
+        if noise is not None and noise.offset_dev is not None:
+            noise.advance_device(G * calls_per_step)
     graph.replay()
     torch.cuda.synchronize()
     return graph, outs, steps // G
@@ -197,11 +201,13 @@ def main():
     row0, row1 = dp.shard_rows(args.batch * world, world, rank)
     B = row1 - row0
     tl, dl = engine_logits(B, g, V, args.sigma, 1000 + rank, dev)
-    step = EngineStep(tl, dl, PhiloxNoise(seed=4242), row0, ops, _lib)
+    # the Philox counter base lives on the device: every replay of the captured steps draws fresh noise
+    noise = PhiloxNoise(seed=4242, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
+    step = EngineStep(tl, dl, noise, row0, ops, _lib)
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
-    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps)
+    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps, noise, g + 1)
     G = len(outs)
     elapsed = timed_replays(graph, replays, dist)
 
@@ -248,11 +254,12 @@ def main():
     if world > 1:
         s0, s1 = dp.shard_rows(args.batch, world, rank)
         stl, sdl = tl[:s1 - s0], dl[:s1 - s0]
-        sstep = EngineStep(stl, sdl, PhiloxNoise(seed=4343), s0, ops, _lib)
+        snoise = PhiloxNoise(seed=4343, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
+        sstep = EngineStep(stl, sdl, snoise, s0, ops, _lib)
         for _ in range(max(args.warmup, 1)):
             sstep()
         torch.cuda.synchronize()
-        sgraph, souts, sreplays = graph_steps(sstep, args.steps, args.graph_steps)
+        sgraph, souts, sreplays = graph_steps(sstep, args.steps, args.graph_steps, snoise, g + 1)
         selapsed = timed_replays(sgraph, sreplays, dist)
         stoks, _ = row_counts(souts, _lib)
         selapsed, stot = dp.aggregate(selapsed, {"tokens": stoks * sreplays}, dev, dist)
@@ -356,7 +363,7 @@ def configs1_lines(dev, args, ops, _lib, PhiloxNoise):
     res = {}
     for name, proc in (("greedy", ops.ProcSpec("greedy")), ("multinomial", ops.ProcSpec("multinomial", 1.0)),
                        ("nucleus_p0.9", ops.ProcSpec("nucleus", 1.0, 0, 0.9))):
-        noise = PhiloxNoise(seed=7)
+        noise = PhiloxNoise(seed=7, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
         draft = torch.zeros(1, g, dtype=torch.long, device=dev)
         dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev)
 
@@ -369,7 +376,7 @@ def configs1_lines(dev, args, ops, _lib, PhiloxNoise):
         for _ in range(5):
             step()
         torch.cuda.synchronize()
-        graph, outs, replays = graph_steps(step, 200, 20)
+        graph, outs, replays = graph_steps(step, 200, 20, noise, g + 1)
         dt = timed_replays(graph, replays, None)
         n = torch.stack([o.n_accepted.long() for o in outs]).sum().item()
         tokens = (n + len(outs)) * replays        # accepted + the resampled / bonus token, every step

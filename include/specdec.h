@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 5
+#define SD_ABI_VERSION 6
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -86,6 +86,9 @@ typedef struct {
     int64_t row_base;        /* PHILOX: global id of row 0 of this call — noise is keyed by
                                 (seed, offset, global row), so a batch sharded across ranks
                                 draws exactly what one call over the whole batch draws     */
+    const uint64_t* offset_dev;  /* PHILOX (nullable): device uint64 added to `offset` when the
+                                kernels run — a captured hipGraph replays with fresh noise once
+                                the caller advances it on the device between replays        */
 } sd_noise;
 
 /* row_status bits */

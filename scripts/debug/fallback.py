@@ -19,7 +19,7 @@ for scale in (1.0, 0.9):
     torch.cuda.synchronize()
     print("scale", scale, "n", out.n_accepted.tolist(), "x", out.next_token.tolist(),
           "st", [hex(s) for s in out.row_status.tolist()], "mass", out.resample_mass.tolist())
-    ws = ops._WS[torch.device("cuda", 0)]
+    ws = next(w for (d, _), w in ops._WS.items() if d == torch.device("cuda", 0))
     # rowstat: after cnt (2*65536*4 B) and part (rows_total*nc float2): print the first floats of each region
     import numpy as np
     raw = ws.cpu().numpy()

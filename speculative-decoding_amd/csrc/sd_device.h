@@ -461,8 +461,9 @@ enum PhiloxSite : uint32_t { kSiteAccept = 1, kSiteSample = 2, kSiteCdf = 3 };
 // counter (idx, global row | site << 24, offset): row is the call-local row, nz.row_base its base
 __device__ __forceinline__ uint4 philox_block(const sd_noise& nz, uint32_t row, uint32_t site, uint32_t idx) {
     const uint32_t grow = (uint32_t)(nz.row_base + row);
-    const uint4 c = make_uint4(idx, (grow & 0x00ffffffu) | (site << 24), (uint32_t)nz.offset,
-                               (uint32_t)(nz.offset >> 32));
+    // offset_dev: a device-resident base added to the call's offset (graph replays move it on the device)
+    const uint64_t off = nz.offset + (nz.offset_dev ? *nz.offset_dev : 0ull);
+    const uint4 c = make_uint4(idx, (grow & 0x00ffffffu) | (site << 24), (uint32_t)off, (uint32_t)(off >> 32));
     return philox4x32_10(c, make_uint2((uint32_t)nz.seed, (uint32_t)(nz.seed >> 32)));
 }
 

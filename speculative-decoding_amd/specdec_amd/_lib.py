@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 5
+SD_ABI_VERSION = 6
 SD_MAX_GAMMA = 16
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
@@ -74,7 +74,8 @@ class sd_processor(C.Structure):
 
 class sd_noise(C.Structure):
     _fields_ = [("mode", C.c_int32), ("words", C.c_void_p), ("n_words", C.c_int64),
-                ("seed", C.c_uint64), ("offset", C.c_uint64), ("row_base", C.c_int64)]
+                ("seed", C.c_uint64), ("offset", C.c_uint64), ("row_base", C.c_int64),
+                ("offset_dev", C.c_void_p)]
 
 
 class sd_verify_args(C.Structure):

@@ -26,6 +26,7 @@ from .. import _lib
 from ..noise import PhiloxNoise, default_noise, noise_session
 from ..ops import PLAIN_SOFTMAX, sample_rows, verify
 from .batch_decode import decode_batch_with_chat_template
+from .graph_window import EngineWindow
 from .metrics import BatchMetrics, RequestMetrics
 
 
@@ -200,13 +201,33 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
     accepted = torch.zeros(B, dtype=torch.long, device=dev)
     stops = torch.tensor(list(ctx.end_tokens), dtype=torch.long, device=dev)
 
+    if isinstance(noise, PhiloxNoise) and getattr(ctx, "drafter_step", None) is not None \
+            and getattr(ctx, "target_rows", None) is not None:
+        # capturable drafter / target steps: the whole window replays from one hipGraph (graph_window.py)
+        if first_token_callback is not None:
+            for idx in range(B):                                          # step 0: every row is active
+                first_token_callback(idx)
+        win = EngineWindow(ctx.drafter_step, ctx.target_rows, input_ids[:, -1], gamma, gen_len, ctx.end_tokens,
+                           noise, row_base=row_base)
+        win.run()
+        noise.offset = win.o0 + win.windows_run * (gamma + 1)             # the calls the windows consumed
+        return _collect(input_ids, win.generated, win.drafted, win.accepted, B)
+
     # perf mode: each draw also returns its row's (max, Σexp), so verify reads only target rows
     stash = isinstance(noise, PhiloxNoise)
     dstats = torch.empty(max(gamma, 1), B, 2, dtype=torch.float32, device=dev) if stash else None
     past = ctx.drafter(input_ids, attention_mask=attention_mask, use_cache=True).past_key_values   # :206
+    # Philox: the all-finished test of :212 is read one window late (pinned copy behind an event), so
+    # the host queues the next window while the GPU runs this one.  A window over all-finished rows
+    # changes nothing, so the outputs are the reference's.  STREAM keeps the exact check: such a
+    # window would still consume generator words.
+    probe = _FinishedProbe(finished) if stash else None
     step = 0
     while step < gen_len:                                                 # :211
-        if bool(finished.all()):
+        if probe is not None:
+            if probe.done():
+                break
+        elif bool(finished.all()):
             break
         gw = min(gamma, gen_len - step)                                   # :216
         draft_tokens = torch.zeros(B, gw, dtype=torch.long, device=dev)
@@ -227,7 +248,7 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
             generated[:, step + d] = torch.where(active, samples, generated[:, step + d])  # :257
             drafted += active.long()                                      # :258
             if first_token_callback is not None and d == 0 and step == 0:
-                for idx in torch.nonzero(active).flatten().tolist():
+                for idx in range(B):                                      # step 0: every row is active
                     first_token_callback(idx)
         verify_ids = torch.cat([input_ids, generated[:, :step + gw]], dim=1).to(target_device)  # :269-270
         t_logits = ctx.target(verify_ids).logits                          # :273
@@ -239,8 +260,39 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
                active=active.to(torch.uint8),
                engine_state=dict(generated=generated, step=step, finished=finished, accepted=accepted),
                row_base=row_base, draft_row_stats=dstats[:gw] if stash and t_logits.device == dev else None)
+        if probe is not None:
+            probe.record()
         step += gw                                                        # :338
+    return _collect(input_ids, generated, drafted, accepted, B)
 
+
+class _FinishedProbe:
+    """finished.all() of the window before last, without a sync on the window just queued."""
+
+    def __init__(self, finished: torch.Tensor):
+        self.finished = finished
+        self.flags = [torch.zeros(1, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        self.events: List[Optional[torch.cuda.Event]] = [None, None]
+        self.w = 0
+
+    def record(self) -> None:
+        i = self.w % 2
+        self.flags[i].copy_((self.finished != 0).all().to(torch.uint8).reshape(1), non_blocking=True)
+        self.events[i] = torch.cuda.Event()
+        self.events[i].record()
+        self.w += 1
+
+    def done(self) -> bool:
+        ev = self.events[self.w % 2]                                      # window w - 2
+        if ev is None:
+            return False
+        ev.synchronize()
+        return bool(self.flags[self.w % 2].item())
+
+
+def _collect(input_ids, generated, drafted, accepted, B):
+    """engine/infer_engine.py:341-357: prompt + generated up to the last nonzero token, per-row rates."""
+    dev = input_ids.device
     gen_host = generated.cpu()
     drafted_h, accepted_h = drafted.tolist(), accepted.tolist()
     outputs, rates = [], []

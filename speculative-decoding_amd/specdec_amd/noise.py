@@ -178,13 +178,26 @@ class StreamNoise:
 
 
 class PhiloxNoise:
+    """Perf-mode noise: Philox4x32-10 keyed by (seed, call offset, global row) in the kernels.
+
+    Every call takes the next host offset.  ``offset_dev`` (optional int64 [1] device tensor) is
+    added to it by the kernels when they run: a hipGraph captures fixed host offsets, and
+    advancing ``offset_dev`` on the device between replays (``advance_device``) gives every
+    replay fresh noise without leaving the graph."""
     mode = _lib.SD_NOISE_PHILOX
 
-    def __init__(self, seed: Optional[int] = None, offset: int = 0):
+    def __init__(self, seed: Optional[int] = None, offset: int = 0, offset_dev: Optional[torch.Tensor] = None):
         if seed is None:   # deterministic under torch.manual_seed
             seed = int(torch.randint(0, 2 ** 62, (1,)).item())
         self.seed = seed & 0xFFFFFFFFFFFFFFFF
         self.offset = offset
+        self.offset_dev = offset_dev
+
+    def advance_device(self, calls: int) -> None:
+        """Move the device base past `calls` host offsets (a stream-ordered add; capturable)."""
+        if self.offset_dev is None:
+            raise ValueError("PhiloxNoise has no offset_dev")
+        self.offset_dev.add_(int(calls))
 
     def next_offset(self) -> int:
         o = self.offset

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -63,16 +63,33 @@ def _stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
-_WS: Dict[torch.device, torch.Tensor] = {}
+# One workspace per (device, stream): it holds the arrival counters and partials of the calls in
+# flight, so calls on different streams must not share one (they would mix their counters).  A
+# workspace is allocated on the stream that uses it, so replacing it by a bigger one is
+# stream-ordered by the caching allocator.  Graph capture reuses the device's largest eager
+# workspace (the capture stream is a side stream; run the call eagerly once before capturing) and
+# keeps it alive for as long as the process runs, since replays hold its address.
+_WS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+_GRAPH_WS: List[torch.Tensor] = []
 
 
 def _workspace(nbytes: int, device) -> torch.Tensor:
     dev = torch.device(device)
-    ws = _WS.get(dev)
+    if torch.cuda.is_current_stream_capturing():
+        cands = [w for (d, _), w in _WS.items() if d == dev]
+        ws = max(cands, key=lambda w: w.numel()) if cands else None
+        if ws is None or ws.numel() < nbytes:
+            raise RuntimeError("specdec: a call captured into a hipGraph needs a workspace sized by an eager call "
+                               "of the same shape first (run it once before capturing)")
+        if not any(w is ws for w in _GRAPH_WS):
+            _GRAPH_WS.append(ws)
+        return ws
+    key = (dev, torch.cuda.current_stream(dev).cuda_stream)
+    ws = _WS.get(key)
     if ws is None or ws.numel() < nbytes:
         # zero-filled once: the library keeps its arrival counters (front of the workspace) at zero
         ws = torch.zeros(max(nbytes, 1 << 20), dtype=torch.uint8, device=dev)
-        _WS[dev] = ws
+        _WS[key] = ws
     return ws
 
 
@@ -92,11 +109,15 @@ def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
     row_base: global id of the call's row 0 (Philox noise is keyed by the global row)."""
     if isinstance(noise, StreamNoise):
         words = noise.prepare(n_words_needed, device)
-        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0, 0), words
+        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0, 0, None), words
     if isinstance(noise, PhiloxNoise):
         if not 0 <= row_base < (1 << 24):
             raise ValueError("row_base must be in [0, 2^24)")
-        return _lib.sd_noise(_lib.SD_NOISE_PHILOX, None, 0, noise.seed, noise.next_offset(), row_base), None
+        od = noise.offset_dev
+        if od is not None and (od.dtype != torch.int64 or od.numel() != 1 or od.device != torch.device(device)):
+            raise ValueError("PhiloxNoise.offset_dev must be an int64 [1] tensor on the call's device")
+        return _lib.sd_noise(_lib.SD_NOISE_PHILOX, None, 0, noise.seed, noise.next_offset(), row_base,
+                             od.data_ptr() if od is not None else None), None
     raise TypeError(f"unsupported noise source {type(noise).__name__}")
 
 

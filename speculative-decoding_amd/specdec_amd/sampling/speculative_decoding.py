@@ -43,11 +43,21 @@ def _cache_len(cache) -> int:
     return int(cache.length)
 
 
-def _forward(model, ids: torch.Tensor, end: int, cache, use_cache: bool):
-    """Run `model` on positions [cached, end) of ids; returns (logits, new cache, first position)."""
-    start = _cache_len(cache) if use_cache else 0
-    out = model(input_ids=ids[..., start:end], past_key_values=cache if use_cache else None, use_cache=use_cache)
-    return out.logits, out.past_key_values, start
+def _forward(model, ids: torch.Tensor, end: int, cache, use_cache: bool, static_len=None):
+    """Run `model` on positions [cached, end) of ids; returns (logits, new cache, first position).
+    static_len: the host's copy of a StaticCache's length (its own is a device tensor, and the
+    positions are passed explicitly, so nothing is read back)."""
+    kw = {}
+    if not use_cache:
+        start = 0
+    elif static_len is not None:
+        start = static_len
+        kw["cache_position"] = torch.arange(start, end, device=ids.device)
+    else:
+        start = _cache_len(cache)
+    out = model(input_ids=ids[..., start:end], past_key_values=cache if use_cache else None, use_cache=use_cache,
+                **kw)
+    return out.logits, (cache if static_len is not None else out.past_key_values), start
 
 
 @torch.no_grad()
@@ -65,16 +75,26 @@ def speculative_generate(
     skip_sample_adjustment: bool = False,
     first_target: bool = True,
     debug: bool = False,
+    static_cache: bool = False,
 ) -> Tuple[List[int], float]:
+    """sampling/speculative_decoding.py:22-189.  One keyword beyond the reference's:
+    static_cache (with use_cache): both models decode into a transformers-5 StaticCache sized for
+    the whole sequence, cropped ON THE DEVICE by the verify kernel's prune outputs (§8f-2)."""
     noise = default_noise()
     with noise_session(noise):   # STREAM: the generator state stays on the device for the loop
         return _speculative_generate(noise, inputs, drafter, target, gamma, logits_processor, max_gen_len,
                                      eos_tokens_id, pad_token_id, use_cache, skip_sample_adjustment, first_target,
-                                     debug)
+                                     debug, static_cache)
+
+
+def _static_caches(drafter, target, total_len):
+    from transformers.cache_utils import StaticCache
+    return (StaticCache(config=drafter.config, max_cache_len=total_len),
+            StaticCache(config=target.config, max_cache_len=total_len))
 
 
 def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processor, max_gen_len, eos_tokens_id,
-                          pad_token_id, use_cache, skip_sample_adjustment, first_target, debug):
+                          pad_token_id, use_cache, skip_sample_adjustment, first_target, debug, static_cache=False):
     spec = proc_spec(logits_processor)
     dev = target.device
     if torch.device(dev).type != "cuda":
@@ -91,9 +111,14 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
     input_ids[0, :prompt_len] = torch.tensor(inputs, dtype=torch.long, device=dev)
     cur = prompt_len
     drafter_cache = target_cache = None
+    static = bool(static_cache and use_cache)
+    dlen = tlen = 0                                              # host copies of the static lengths
+    if static:
+        drafter_cache, target_cache = _static_caches(drafter, target, total_len)
 
     if first_target:                                             # :84-103
-        logits, target_cache, _ = _forward(target, input_ids, cur, target_cache, use_cache)
+        logits, target_cache, _ = _forward(target, input_ids, cur, target_cache, use_cache, tlen if static else None)
+        tlen = cur
         sample_rows(logits[:, -1, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1])
         t = int(input_ids[0, cur].item())
         cur += 1
@@ -108,14 +133,18 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         ids_d = input_ids.to(drafter.device)
         draft_rows = []
         for k in range(g):                                       # :112-124
-            logits, drafter_cache, _ = _forward(drafter, ids_d, cur + k, drafter_cache, use_cache)
+            logits, drafter_cache, _ = _forward(drafter, ids_d, cur + k, drafter_cache, use_cache,
+                                                dlen if static else None)
+            dlen = cur + k
             row = logits[:, -1, :]
             sample_rows(row, spec, noise, tokens_out=ids_d[0, cur + k:cur + k + 1],
                         row_stats_out=dstats[k] if stash else None)
             draft_rows.append(row if row.device == torch.device(dev) else row.to(dev))
         drafts_speculated += g
         input_ids = ids_d.to(dev)
-        logits, target_cache, start = _forward(target, input_ids, cur + g, target_cache, use_cache)
+        logits, target_cache, start = _forward(target, input_ids, cur + g, target_cache, use_cache,
+                                               tlen if static else None)
+        tlen = cur + g
         if g == 0:
             # last position: rand(0) draws nothing, n = 0 = γ', the bonus row is sampled (:158-171)
             sample_rows(logits[:, cur - 1 - start, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1])
@@ -137,7 +166,12 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         drafts_accepted += n                                     # :147
         if status & _lib.SD_ROW_STOP_IN_DRAFTS:                  # :150-155
             return input_ids[0, prompt_len:cur + stop_index + 1].tolist(), drafts_accepted / drafts_speculated
-        if n < g and use_cache:                                  # :163-165
+        if static:                                               # :163-165 on the device (0 = no-op)
+            prune_cache(drafter_cache, out.prune_drafter)
+            prune_cache(target_cache, out.prune_target)
+            if n < g:
+                dlen, tlen = dlen - (g - n), tlen - (g - n + 1)
+        elif n < g and use_cache:                                # :163-165
             drafter_cache = prune_cache(drafter_cache, g - n)
             target_cache = prune_cache(target_cache, g - n + 1)
         input_ids[0, cur + n:cur + g] = pad_token_id             # :176-177

@@ -1,6 +1,7 @@
 """KV-cache prune (utils/caching.py:6-77).
 
-The prune is metadata-only: drop the last k positions of every K/V tensor.  The verify kernel
+The prune is metadata-only: drop the last k positions of every K/V tensor.  A transformers-5
+StaticCache is cropped ON THE DEVICE by the verify kernel's prune output (prune_static_cache).  The verify kernel
 returns k per sequence (prune_drafter = γ'-n, prune_target = γ'-n+1,
 sampling/speculative_decoding.py:163-165).  Unlike the reference, the DynamicCache branch works
 on transformers 5.x (the reference reads the removed ``key_cache``/``_seen_tokens``):
@@ -14,6 +15,7 @@ from __future__ import annotations
 
 from typing import Tuple, Union
 
+import torch
 from torch import Tensor
 
 try:  # transformers is optional for the tuple path
@@ -22,10 +24,29 @@ except Exception:  # pragma: no cover
     DynamicCache = None
 
 
-def prune_cache(cache, num_tokens_to_discard: int):
-    """utils/caching.py:6-24: tuple caches -> views, cache objects -> cropped in place."""
+def _static_lengths(cache):
+    """The per-layer device length tensors of a transformers-5 StaticCache (StaticLayer keeps the
+    cached length as a device tensor, ``cumulative_length``, and writes new keys at it), or None."""
+    layers = getattr(cache, "layers", None)
+    if not layers:
+        return None
+    lens = [getattr(layer, "cumulative_length", None) for layer in layers]
+    if not all(torch.is_tensor(t) for t in lens):
+        return None
+    return lens
+
+
+def prune_cache(cache, num_tokens_to_discard: Union[int, Tensor]):
+    """utils/caching.py:6-24: tuple caches -> views, cache objects -> cropped in place.
+
+    num_tokens_to_discard may be a device tensor (the verify kernel's ``prune_*`` output) for a
+    StaticCache: the crop then runs on the device, driven by the kernel, with no host read."""
     if cache is None:
         return None
+    if _static_lengths(cache) is not None:
+        return prune_static_cache(cache, num_tokens_to_discard)
+    if torch.is_tensor(num_tokens_to_discard):
+        num_tokens_to_discard = int(num_tokens_to_discard.reshape(-1)[0].item())   # host crop: one read
     if isinstance(cache, tuple):
         return prune_tuple_cache(cache, num_tokens_to_discard)
     if (DynamicCache is not None and isinstance(cache, DynamicCache)) or hasattr(cache, "crop"):
@@ -54,3 +75,23 @@ def prune_dynamic_cache(cache, num_tokens_to_discard: int):
     if num_tokens_to_discard > 0:
         cache.crop(-int(num_tokens_to_discard))
     return cache
+
+
+def prune_static_cache(cache, num_tokens_to_discard: Union[int, Tensor]):
+    """Device-side crop of a transformers-5 StaticCache: the K/V buffers keep
+    their addresses and the stale positions are overwritten by the next write (the causal mask
+    built from ``cache_position`` hides them meanwhile), so dropping the last k positions is
+    ``cumulative_length -= k`` in every layer — one multi-tensor launch.  k is an int, or a device
+    tensor of one element (batch 1, as the reference's prune; ``prune_*[0]`` of a verify), which
+    keeps the crop on the device without a host read.  k = 0 is a no-op, so a loop can apply the
+    kernel's prune output every step without branching on it."""
+    lens = _static_lengths(cache)
+    if lens is None:
+        raise ValueError("not a StaticCache")
+    if torch.is_tensor(num_tokens_to_discard):
+        k = num_tokens_to_discard.reshape(-1)[:1].reshape(())
+        torch._foreach_sub_(lens, k.to(device=lens[0].device, dtype=lens[0].dtype))
+    elif num_tokens_to_discard:
+        torch._foreach_sub_(lens, int(num_tokens_to_discard))
+    return cache
+
