@@ -15,6 +15,7 @@ All compute goes through libspecdec.so (HIP, gfx950); importing fails if it is m
 from . import _lib  # noqa: F401  (loads libspecdec.so or raises)
 from .noise import PhiloxNoise, StreamNoise, default_noise, set_noise_mode  # noqa: F401
 from .ops import ProcSpec, proc_spec, probs_rows, sample_rows, verify  # noqa: F401
+from . import torch_ops  # noqa: F401,E402  (registers torch.ops.specdec.sample / .verify)
 
 __all__ = ["PhiloxNoise", "StreamNoise", "default_noise", "set_noise_mode", "ProcSpec", "proc_spec",
            "probs_rows", "sample_rows", "verify"]

@@ -177,3 +177,31 @@ def test_workspaces_are_per_stream():
     for a, b in zip(want, got):
         assert torch.equal(a.n_accepted, b.n_accepted) and torch.equal(a.next_token, b.next_token)
         assert torch.equal(a.row_status, b.row_status)
+
+
+def test_torch_library_ops_equal_the_python_api():
+    from specdec_amd import PhiloxNoise, _lib, ops
+    g = torch.Generator(device=DEV).manual_seed(12)
+    B, gam, V = 8, 4, 50257
+    tl = (torch.randn(B, gam + 1, V, generator=g, device=DEV) * 3).to(torch.bfloat16)
+    dl = (tl[:, :gam].float() + torch.randn(B, gam, V, generator=g, device=DEV)).to(torch.bfloat16)
+    tok, stats, st = torch.ops.specdec.sample(dl[:, 0], 1, 1.0, 0, 1.0, 5, 3, 0)
+    want_stats = torch.empty(B, 2, device=DEV)
+    want, _, _ = ops.sample_rows(dl[:, 0], ops.ProcSpec("multinomial"), PhiloxNoise(5, 3), row_stats_out=want_stats)
+    assert torch.equal(tok, want) and torch.equal(stats, want_stats)
+    draft = torch.randint(0, V, (B, gam), generator=g, device=DEV)
+    stops = torch.tensor([1, 2], dtype=torch.long, device=DEV)
+    got = torch.ops.specdec.verify(tl, dl, draft, stops, _lib.SD_RULE_SPEC, 3, 0.8, 0, 0.9, 9, 1, 0)
+    spec = ops.ProcSpec("nucleus", 0.8, 0, 0.9)
+    ref = ops.verify([tl[:, t] for t in range(gam + 1)], [dl[:, d] for d in range(gam)], draft, _lib.SD_RULE_SPEC,
+                     spec, spec, PhiloxNoise(9, 1), stops)
+    for a, b in zip(got, (ref.n_accepted, ref.next_token, ref.resample_mass, ref.prune_drafter, ref.prune_target,
+                          ref.stop_index, ref.row_status)):
+        assert torch.equal(a, b) or (a.dtype == torch.float32 and torch.equal(a.isnan(), b.isnan()))
+
+    # traced by torch.compile (aot_eager: fake-tensor tracing through register_fake, no inductor)
+    def engine_verify(t, d, ids):
+        return torch.ops.specdec.verify(t, d, ids, stops, _lib.SD_RULE_ENGINE, 1, 1.0, 0, 1.0, 21, 0, 0)[0]
+    eager = engine_verify(tl[:, :gam], dl, draft)
+    compiled = torch.compile(engine_verify, backend="aot_eager", fullgraph=True)(tl[:, :gam], dl, draft)
+    assert torch.equal(eager, compiled)
