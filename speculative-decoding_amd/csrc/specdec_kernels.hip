@@ -1916,7 +1916,43 @@ __device__ __forceinline__ uint32_t draw_tag(uint32_t epoch, int r, int c, int n
     return h | 1u;   // never 0 (zero-filled workspace)
 }
 
+// GREEDY (argmax of the rounded probabilities, first index on ties — GreedyProcessor.sample on
+// softmax(l) in the row's dtype, utils/logits_processor.py:26-36) in the same single pass: the
+// rounded probability is monotone in the logit, so the winner lies in a span whose max m_c rounds
+// to the row's top probability P* = p(M).  Each span publishes m_c, the first index of m_c, and
+// whether any OTHER value lies strictly within kGreedyDelta below m_c (two probabilities that round
+// to one bf16 value differ by < 2^-7 relative, e^-0.0079; fp16 subnormal tops of flat rows at
+// V <= 256 Ki by < 1.6%; kGreedyDelta = 1/32 leaves a margin for both).  The
+// tail takes the first index of every clean qualifying span; a qualifying span with such close
+// values (rare) is rescanned by the tail wave with the exact rule, and so is the whole row when
+// its normaliser is not finite (NaN / inf logits).
+constexpr float kGreedyDelta = 1.0f / 32.0f;
+
 template <int DT, int NST>
+__device__ int greedy_rescan(const DrawLean& A, const char* row, int c, float M, float S) {
+    constexpr int VEC = 8, STEP = kThreads * VEC, SPAN = NST * STEP, PER = SPAN / kWave;
+    const int lane = threadIdx.x & 63;
+    const int64_t base = (int64_t)c * SPAN;
+    const float inv = 1.0f / S;
+    float bv = -INFINITY;
+    int32_t bi = INT_MAX;
+    for (int k0 = 0; k0 < PER; k0 += VEC) {
+        const int64_t e0 = base + (int64_t)lane * PER + k0;   // lane-contiguous runs: index order per lane
+        float x[VEC];
+        load_vec<DT>(row, e0, A.V, true, x);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            const int64_t j = e0 + k;
+            if (j >= A.V) continue;
+            const float p = prob_exact<DT>(x[k], M, S, inv);
+            if (arg_better(p, (int32_t)j, bv, bi)) { bv = p; bi = (int32_t)j; }
+        }
+    }
+    wave_argmax(bv, bi);
+    return bi;
+}
+
+template <int DT, int NST, bool GREEDY = false>
 __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     constexpr int VEC = 8, STEP = kThreads * VEC, EPT = NST * VEC, NW = kThreads / kWave;
     const int c = blockIdx.x, r = blockIdx.y;
@@ -1948,10 +1984,11 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     __shared__ double l_u;
     __shared__ int32_t l_j;
     __shared__ float l_y;
+    __shared__ int32_t l_fi[NW], l_dirty[NW];
     uint32_t epoch = 0;   // poll mode: this launch's epoch of row r (read by wave 0, beside the loads)
     if (w == 0) {   // the span's in-chunk uniform: one wave's scalar unit, while the loads fly
         if (A.poll) epoch = __hip_atomic_load(seq_counter(A.cnt, 2, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const double u = cdf_uniform(A.noise, (uint32_t)r, 1u + (uint32_t)c);
+        const double u = GREEDY ? 0.0 : cdf_uniform(A.noise, (uint32_t)r, 1u + (uint32_t)c);
         if (lane == 0) { l_u = u; l_j = -1; l_y = -INFINITY; }
     }
     // per-wave max and weights: no barrier before the exps
@@ -1985,9 +2022,25 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         off += Wk;
     }
     const float T = off;
+    if constexpr (GREEDY) {
+        // first index of the span max and whether another value lies within kGreedyDelta of it
+        int32_t fi = INT_MAX;
+        bool dirty = false;
+#pragma unroll
+        for (int k = 0; k < EPT; ++k) {
+            const int v = k / VEC;
+            const int32_t j = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + (k - v * VEC));
+            if (y[k] == m && fi == INT_MAX) fi = j;
+            dirty |= y[k] > m - kGreedyDelta && y[k] != m;
+        }
+        fi = wave_min_i(fi);
+        const bool dw = __ballot(dirty) != 0;
+        if (lane == 0) { l_fi[w] = fi; l_dirty[w] = dw; }
+    }
     const float t = (float)(l_u * (double)T);
     // the claiming wave (rounding past the end: the last wave with weight)
-    const bool claim = my_W > 0.f && ((t >= my_off && t < my_off + my_W) || (w == lastw && t >= my_off + my_W));
+    const bool claim = !GREEDY && my_W > 0.f &&
+                       ((t >= my_off && t < my_off + my_W) || (w == lastw && t >= my_off + my_W));
     if (claim) {
         const float a = fmaf(incl, my_sc, my_off), a0 = lane == 0 ? my_off : fmaf(prev, my_sc, my_off);
         const uint64_t hit = __ballot(a > t && tl > 0.f), posm = __ballot(tl > 0.f);
@@ -2018,8 +2071,16 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     if (w != 0) return;
     const bool bad = T != T;   // NaN / +inf in the span: S_c NaN flags the row
     const float m_pub = bad && !(m > -INFINITY) ? 0.f : m, s_pub = bad ? NAN : T;
-    const int32_t j_pub = l_j;
-    const float y_pub = l_y;
+    int32_t j_pub = l_j;
+    float y_pub = l_y;
+    int32_t g_dirty = 0;   // GREEDY: another value within kGreedyDelta of the span max
+    if constexpr (GREEDY) {
+        j_pub = l_fi[0];
+        for (int k = 1; k < NW; ++k) j_pub = l_fi[k] < j_pub ? l_fi[k] : j_pub;
+        for (int k = 0; k < NW; ++k) g_dirty |= l_dirty[k];
+        if (j_pub == INT_MAX) j_pub = -1;
+        y_pub = m;
+    }
     float4* part_row = A.part + (int64_t)r * A.pstride;
     int32_t xstat = 0;
     if (A.poll) {
@@ -2033,7 +2094,8 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
                 const uint32_t yraw = DT == SD_BF16 ? (__float_as_uint(y_pub) >> 16)
                                                     : (uint32_t)__half_as_ushort(__float2half_rn(y_pub));
                 const uint32_t off = j_pub >= 0 ? (uint32_t)(j_pub - base) + 1u : 0u;   // <= NST * 2048
-                st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), off | (yraw << 16), tag));
+                const uint32_t gd = GREEDY && g_dirty ? 0x8000u : 0u;
+                st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), off | gd | (yraw << 16), tag));
             }
             return;
         }
@@ -2043,7 +2105,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         uint32_t last = 0;
         if (threadIdx.x == 0) {
             st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), (uint32_t)j_pub,
-                                              __float_as_uint(y_pub)));
+                                              GREEDY ? (uint32_t)g_dirty : __float_as_uint(y_pub)));
             last = arrive_last(seq_counter(A.cnt, 0, r), (uint32_t)A.n_span) ? 1u : 0u;
         }
         if (!__builtin_amdgcn_readlane(last, 0)) return;
@@ -2054,8 +2116,9 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     float M = -INFINITY;
     float mk[2], sk[2], yk[2];
     int32_t jk[2];
+    bool dk[2] = {false, false};   // GREEDY: the span's dirty flag
     const int npass = (A.n_span + kWave - 1) / kWave;   // <= 2 (host: n_span <= 128)
-    const double u_row = cdf_uniform(A.noise, (uint32_t)r);   // scalar unit, before the wait
+    const double u_row = GREEDY ? 0.0 : cdf_uniform(A.noise, (uint32_t)r);   // scalar unit, before the wait
     if (A.poll) {
         // every other span's record, re-read until its tag is this launch's; this span's own from
         // registers (the lane that would hold it)
@@ -2087,10 +2150,11 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             const int k = q * kWave + lane;
             mk[q] = -INFINITY; sk[q] = 0.f; yk[q] = -INFINITY; jk[q] = -1;
             if (k == c) {
-                mk[q] = m_pub; sk[q] = s_pub; jk[q] = j_pub; yk[q] = y_pub;
+                mk[q] = m_pub; sk[q] = s_pub; jk[q] = j_pub; yk[q] = y_pub; dk[q] = g_dirty != 0;
             } else if (q < npass && k < A.n_span && have[q]) {
                 mk[q] = __uint_as_float(rec[q].x); sk[q] = __uint_as_float(rec[q].y);
-                const uint32_t off = rec[q].z & 0xffffu, yraw = rec[q].z >> 16;
+                dk[q] = GREEDY && (rec[q].z & 0x8000u) != 0;
+                const uint32_t off = rec[q].z & (GREEDY ? 0x7fffu : 0xffffu), yraw = rec[q].z >> 16;
                 jk[q] = off ? (int32_t)((int64_t)k * NST * STEP + off - 1) : -1;
                 yk[q] = DT == SD_BF16 ? __uint_as_float(yraw << 16) : __half2float(__ushort_as_half((unsigned short)yraw));
             }
@@ -2104,7 +2168,8 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         if (q < npass && k < A.n_span) {
             const uint4 v = ld_coh16(pr + 2 * k);
             mk[q] = __uint_as_float(v.x); sk[q] = __uint_as_float(v.y);
-            jk[q] = (int32_t)v.z; yk[q] = __uint_as_float(v.w);
+            jk[q] = (int32_t)v.z; yk[q] = GREEDY ? mk[q] : __uint_as_float(v.w);
+            dk[q] = GREEDY && v.w != 0u;
         }
         M = fmaxf(M, mk[q]);
     }
@@ -2117,6 +2182,52 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         S += wk[q];
     }
     S = wave_sum(S);
+    if constexpr (GREEDY) {
+        const bool ok = S > 0.f && S != INFINITY && M == M;
+        const float inv = 1.0f / S;
+        const float pst = ok ? prob_exact<DT>(M, M, S, inv) : 0.f;
+        int32_t cand = INT_MAX;
+        bool resc[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = q * kWave + lane;
+            const bool in = q < npass && k < A.n_span;
+            const bool qual = in && (!ok || (mk[q] > -INFINITY && prob_exact<DT>(mk[q], M, S, inv) == pst));
+            resc[q] = qual && (!ok || dk[q] || jk[q] < 0);
+            if (qual && !resc[q]) cand = jk[q] < cand ? jk[q] : cand;
+        }
+        cand = wave_min_i(cand);
+        // rescans (rare): the exact rule over each flagged span; an invalid row is scanned whole
+        float bv = -INFINITY;
+        int32_t bi = INT_MAX;
+        if (cand != INT_MAX) { bv = ok ? pst : -INFINITY; bi = cand; }
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            uint64_t mask = __ballot(resc[q]);
+            while (mask) {
+                const int k = q * kWave + __builtin_ctzll(mask);
+                mask &= mask - 1;
+                const int32_t j = greedy_rescan<DT, NST>(A, row, k, M, S);
+                if (j != INT_MAX) {
+                    const float pv = prob_exact<DT>(load_one<DT>(row, j), M, S, inv);
+                    if (arg_better(pv, j, bv, bi)) { bv = pv; bi = j; }
+                }
+            }
+        }
+        const int32_t x = bi == INT_MAX ? -1 : bi;
+        if (lane == 0) {
+            int32_t st = SD_ROW_DONE | xstat;
+            if (!ok) st |= SD_ROW_INVALID_DIST;
+            if (x < 0) st |= SD_ROW_INVALID_DIST;
+            if (A.poll) __hip_atomic_store(seq_counter(A.cnt, 2, r), epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            A.next_token[r * A.nt_stride] = x;
+            if (A.token_prob) A.token_prob[r] = x >= 0 ? bv : NAN;
+            if (A.row_stats) A.row_stats[r] = make_float2(M, S);
+            if (A.row_status) A.row_status[r] = st;
+            if (r == 0 && A.words_used) *A.words_used = 0;
+        }
+        return;
+    }
     // span pick: first span whose fp64 running total (span order) exceeds u * Σ
     double base_d = 0.0, tot = 0.0;
 #pragma unroll
@@ -2409,7 +2520,7 @@ int32_t launch_draw_dt(const sd::Plan& P, int nst, void* stream) {
 }
 
 // k_draw_lean's cases: T = 1, no processor, 16-bit rows, every row 16-byte aligned, <= 128 spans
-template <int DT, int NST>
+template <int DT, int NST, bool GREEDY = false>
 int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
     DrawLean A{};
     A.rows = static_cast<const char*>(P.trow[0]);
@@ -2429,15 +2540,28 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
     if (cap[dev] == 0) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_draw_lean<DT, NST>, kThreads, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_draw_lean<DT, NST, GREEDY>, kThreads, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             per_cu = cus = 0;
         cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
     }
     static const bool no_poll = getenv("SD_DRAW_NO_POLL") != nullptr;   // A/B switch: counter mode only
     A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && !no_poll;
-    SD_LAUNCH((k_draw_lean<DT, NST>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
+    SD_LAUNCH((k_draw_lean<DT, NST, GREEDY>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
     return SD_OK;
+}
+
+// greedy sd_sample rows in one pass (k_draw_lean<GREEDY>): 1 if launched, 0 if the shape needs the
+// three-launch path (statistics, per-chunk argmax, finalize), < 0 on a launch error
+int32_t launch_greedy_lean(const sd::Plan& P, void* stream) {
+    static const bool off = getenv("SD_GREEDY_LEAN") && atoi(getenv("SD_GREEDY_LEAN")) == 0;   // A/B switch
+    const bool fast = P.tT == 1.0f && !P.t_keep && P.tdt != SD_F32;
+    const bool al = (reinterpret_cast<uintptr_t>(P.trow[0]) & 15) == 0 && (P.tstride * 2) % 16 == 0;
+    const int64_t span = (int64_t)kThreads * 8;
+    if (off || !fast || !al || P.V < 8 || (P.V + span - 1) / span > 128) return 0;
+    const int32_t st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 1, true>(P, stream)
+                                        : launch_draw_lean_t<SD_F16, 1, true>(P, stream);
+    return st == SD_OK ? 1 : st;
 }
 
 int32_t launch_draw(sd::Plan& P, void* stream) {
@@ -2630,6 +2754,11 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     if (P.noise.mode == SD_NOISE_PHILOX && P.t_stoch) {
         if (P.B > kCntMax || max_chunks(P.V) > kTailChunks) return SD_ERR_UNSUPPORTED;
         return launch_draw(P, stream);   // one pass; the row's last arrival writes the outputs
+    }
+    if (!P.t_stoch && P.B <= kCntMax) {   // greedy (either noise mode: no noise is drawn)
+        const int32_t st = launch_greedy_lean(P, stream);
+        if (st < 0) return st;
+        if (st == 1) return SD_OK;
     }
     set_rchunks(P);
     if (int32_t st = launch_stats(P, stream)) return st;
