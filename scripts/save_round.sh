@@ -16,7 +16,7 @@ b = json.load(open(f"profiles/{tag}_bench.json"))
 rows = list(csv.DictReader(open(f"profiles/{tag}_kernel_stats_step_draws_verify.csv")))
 k = b["roofline"]["kernel"]
 for r in rows:
-    if f"sd::{k}<" in r["Name"]:
+    if f"sd::{k}<" in r["Name"] or f"sd::{k}_lean<" in r["Name"]:
         print(f"{k}: bench {b['roofline']['kernel_ms']*1e6:.0f} ns/launch, rocprof avg {float(r['AverageNs']):.0f} ns "
               f"({r['Calls']} calls)")
 print("value", b["value"], "ms/step", b["ms_per_step"], "frac", b["roofline"]["frac"])
