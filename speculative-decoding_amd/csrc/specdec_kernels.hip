@@ -24,6 +24,8 @@
 #include <climits>
 #include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <type_traits>
 
 #include "sd_device.h"
@@ -111,6 +113,7 @@ struct Plan {
     int32_t coh;          // partials may come from the same launch: read them agent-coherently
     int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
     int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
+    int32_t spoll;        // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
     // sd_ngram_verify (sd_ngram.inc)
     struct NgPart* ngpart;
     int64_t* filler_ids;
@@ -1277,6 +1280,15 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
     }
 }
 
+// Poll-mode tag of k_sample's chunk record c of sequence b (k_draw_lean's protocol): the sequence's
+// epoch (counter set 3, advanced by its consumer after every call) hashed with b and c, salted
+// apart from k_draw_lean's row records, which share the region.
+__device__ __forceinline__ uint32_t sample_tag(uint32_t epoch, int b, int c) {
+    uint32_t h = epoch * 0x9E3779B1u + (uint32_t)b * 0x85EBCA77u + (uint32_t)c * 0xC2B2AE3Du + 0x5A3B1E7Du;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;   // murmur3 fmix32
+    return h | 1u;   // never 0 (the counter path's records carry 0)
+}
+
 // Perf-mode sampling is a two-level inverse CDF.  Each sampling chunk c draws its own candidate
 // j_c with an independent Philox U'_c (chunk_pick, on the weights it holds in registers); the
 // sequence's tail then picks the chunk on the fp64 running sum of the chunk totals with U
@@ -1417,7 +1429,7 @@ __device__ __forceinline__ int pick_chunk(const Plan& P, double u, const float* 
 // load.  Only the engine's den <= 1e-12 fallback re-reads a chunk (its p weights).
 template <int TDT, int DDT, bool FAST, bool STOCH>
 __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, int b, PairRows R, double u_row,
-                                              int wg_id) {
+                                              int wg_id, const uint32_t* poll_epoch = nullptr) {
     constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
@@ -1430,6 +1442,9 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
     int64_t x = -1;
     float mass = NAN;
     int32_t status = d.status;
+    __shared__ int32_t s_xstat;   // poll mode: a record that never arrived
+    if (threadIdx.x == 0) s_xstat = 0;
+    if (poll_epoch) __syncthreads();
     if constexpr (STOCH) {
         __shared__ float l_sum[kTailChunks], l_pv[kTailChunks];
         __shared__ int32_t l_cand[kTailChunks];
@@ -1437,7 +1452,15 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
         if (d.mode != kModeNone) {
             const float4* rp = reinterpret_cast<const float4*>(P.rpart) + (int64_t)b * P.rn_chunks;
             for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
-                const uint4 v = ld_coh16(rp + k);
+                uint4 v = ld_coh16(rp + k);
+                if (poll_epoch) {   // poll mode: re-read until the record carries this call's tag (bounded)
+                    const uint32_t tag = sample_tag(*poll_epoch, b, k);
+                    for (int spin = 0; v.w != tag; ++spin) {
+                        if (spin >= (1 << 16)) { atomicOr(&s_xstat, SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST); break; }
+                        __builtin_amdgcn_s_sleep(1);
+                        v = ld_coh16(rp + k);
+                    }
+                }
                 l_sum[k] = __uint_as_float(v.x);
                 l_pv[k] = __uint_as_float(v.y);
                 l_cand[k] = (int32_t)v.z;
@@ -1482,6 +1505,10 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
     } else {
         if (d.mode != kModeNone && threadIdx.x < kWave) pick_wave(P, b, d, x, mass, status);
     }
+    if (poll_epoch) {
+        __syncthreads();
+        status |= s_xstat;
+    }
     if (threadIdx.x == 0) finalize_write(P, b, d, x, mass, status, acc0, lstops);
     SD_TS(wg_id, 6);
 }
@@ -1490,6 +1517,33 @@ __device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
     Decision d = P.dec[b];
     if (d.mode < kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) d.mode = kModeNone;
     return d;
+}
+
+// Stochastic sampling chunk c of sequence b (whole workgroup): the chunk's Σ weight, Σ p, and its own
+// inverse-CDF candidate (pick_chunk's comment), published as one 16-byte record (k_draw's layout;
+// .w = the poll-mode tag, or 0).
+template <int TDT, int DDT, bool FAST>
+__device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, int b, int c, uint32_t tag) {
+    constexpr int EPT = 8;
+    constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
+    const double u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
+    float psum = 0.f;
+    const int64_t base = (int64_t)c * P.rchunk;
+    float wv[EPT];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        float pv[VEC];
+        pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv + v * VEC, pv);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) psum += pv[k];
+    }
+    double T;
+    float PT;
+    const int pos = chunk_pick<EPT>(wv, u, psum, T, PT);
+    if (threadIdx.x == 0)   // {Σ w, Σ p, candidate, tag}
+        st_coh16(reinterpret_cast<float4*>(P.rpart) + (int64_t)b * P.rn_chunks + c,
+                 make_uint4(__float_as_uint((float)T), __float_as_uint(PT),
+                            (uint32_t)(pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos)), tag));
 }
 
 // grid (chunk, B).  STOCH: chunk Σ weight; greedy (!STOCH): the exact argmax-candidate bodies.
@@ -1502,7 +1556,6 @@ __device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
 template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL, bool DEC = false>
 __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     constexpr int EPT = 8;
-    constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const int wg_id = 8192 + blockIdx.y * gridDim.x + blockIdx.x;
     int b, c;
     if (P.xcd_affine) affine_split(wg_id - 8192, (int)gridDim.x, b, c);
@@ -1526,31 +1579,17 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     }
     // the tail's chunk-pick uniform, computed while the decision load is in flight
     const double u_row = STOCH && TAIL ? cdf_uniform(P.noise, (uint32_t)b) : 0.0;
+    // poll mode (stochastic tails): this call's epoch of sequence b, read beside the decision load
+    const bool poll = STOCH && TAIL && !DEC && P.spoll;
+    uint32_t epoch = 0;
+    if (poll) epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PairRows R{};
     if (d.mode != kModeNone) {
         if constexpr (STOCH) {
             // RESID also sums p: the engine's den <= 1e-12 fallback samples the target row itself
             R = pair_rows<TDT, DDT>(P, d, b);
             SD_TS(wg_id, 1);
-            // chunk Σ weight, Σ p, and the chunk's own inverse-CDF candidate (pick_chunk's comment)
-            const double u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
-            float psum = 0.f;
-            const int64_t base = (int64_t)c * P.rchunk;
-            float wv[EPT];
-#pragma unroll
-            for (int v = 0; v < NV; ++v) {
-                float pv[VEC];
-                pair_weights<TDT, DDT, FAST>(R, base + ((int64_t)v * kThreads + threadIdx.x) * VEC, wv + v * VEC, pv);
-#pragma unroll
-                for (int k = 0; k < VEC; ++k) psum += pv[k];
-            }
-            double T;
-            float PT;
-            const int pos = chunk_pick<EPT>(wv, u, psum, T, PT);
-            if (threadIdx.x == 0)   // {Σ w, Σ p, candidate}: one 16-byte record per chunk (k_draw's layout)
-                st_coh16(reinterpret_cast<float4*>(P.rpart) + (int64_t)b * P.rn_chunks + c,
-                         make_uint4(__float_as_uint((float)T), __float_as_uint(PT),
-                                    (uint32_t)(pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos)), 0u));
+            sample_chunk<TDT, DDT, FAST>(P, R, b, c, poll ? sample_tag(epoch, b, c) : 0u);
         } else {
             const float2 mst = P.rowstat[b * P.slots + d.slot];
             const float2 msd = d.mode == kModeResid && !P.draft_is_probs ? P.rowstat[b * P.slots + P.n_tslots + d.slot]
@@ -1561,6 +1600,18 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     }
     SD_TS(wg_id, 2);
     if constexpr (TAIL) {
+        if (poll) {
+            // the sequence's last chunk (the ragged one: least work) is its consumer; the others
+            // have published their records and are done — no counter, no write-ack wait
+            if (c != P.rn_chunks - 1) return;
+            __shared__ uint32_t s_epoch;
+            if (threadIdx.x == 0) s_epoch = epoch;
+            __syncthreads();
+            sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, u_row, wg_id, &s_epoch);
+            if (threadIdx.x == 0)
+                __hip_atomic_store(seq_counter(P.cnt, 3, b), epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
         __shared__ int s_last;
         if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 1, b), (uint32_t)P.rn_chunks);
         __syncthreads();
@@ -2333,7 +2384,9 @@ int max_chunks(int vocab) { return (vocab + kThreads * kEptSmall - 1) / (kThread
 
 void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     const int nc = max_chunks(vocab);
-    P.cnt = c.take<uint32_t>(3 * (size_t)kCntMax * kCntStride);   // first, at a fixed offset (see kCntMax)
+    // first, at a fixed offset (see kCntMax): sets 0 / 1 arrivals, 2 k_draw_lean row epochs,
+    // 3 k_sample poll-mode sequence epochs
+    P.cnt = c.take<uint32_t>(4 * (size_t)kCntMax * kCntStride);
     P.part = c.take<float2>((size_t)rows_total * nc);
     P.rowstat = c.take<float2>(rows_total);
     P.keep = c.take<RowKeep>(rows_total);
@@ -2417,6 +2470,28 @@ int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, in
     return launch_stats_dt<SD_F16, false>(P, fast, slot_lo, slot_cnt, stream);
 }
 
+// k_sample's poll-mode finish needs its B consumers plus at least one producer resident: B < the
+// kernel's resident capacity (occupancy x CUs, per device and kernel, queried once); SD_SAMPLE_POLL=0
+// keeps the arrival counter (A/B)
+bool sample_poll_ok(int B, const void* kern) {
+    static const bool off = getenv("SD_SAMPLE_POLL") && atoi(getenv("SD_SAMPLE_POLL")) == 0;
+    if (off) return false;
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> caps;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = caps.find({dev, kern});
+    if (it == caps.end()) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = cus = 0;
+        it = caps.emplace(std::make_pair(dev, kern), per_cu * cus).first;
+    }
+    return 2 * B <= it->second;
+}
+
 template <int TDT, int DDT>
 int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
     const dim3 grid(P.rn_chunks, P.B);
@@ -2431,8 +2506,12 @@ int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
             else SD_LAUNCH((k_sample<TDT, DDT, false, true, true, true>), grid, dim3(kThreads), stream, P);
         } else if (P.tails) {
             if (P.t_stoch) {
-                if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true>), grid, dim3(kThreads), stream, P);
-                else SD_LAUNCH((k_sample<TDT, DDT, false, true, true>), grid, dim3(kThreads), stream, P);
+                // poll-mode finish when the consumers (one per sequence) leave room for every producer
+                sd::Plan Q = P;
+                Q.spoll = sample_poll_ok(P.B, fast ? (const void*)k_sample<TDT, DDT, true, true, true>
+                                                   : (const void*)k_sample<TDT, DDT, false, true, true>);
+                if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true>), grid, dim3(kThreads), stream, Q);
+                else SD_LAUNCH((k_sample<TDT, DDT, false, true, true>), grid, dim3(kThreads), stream, Q);
             } else {
                 if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, false, true>), grid, dim3(kThreads), stream, P);
                 else SD_LAUNCH((k_sample<TDT, DDT, false, false, true>), grid, dim3(kThreads), stream, P);
