@@ -114,6 +114,7 @@ struct Plan {
     int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
     int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
     int32_t spoll;        // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
+    int32_t kpoll;        // k_stats (decide tail): poll-mode partials (tagged records, no counter)
     // sd_ngram_verify (sd_ngram.inc)
     struct NgPart* ngpart;
     int64_t* filler_ids;
@@ -303,7 +304,18 @@ __device__ __forceinline__ void pf_late(const Plan& P, int b, int i, DraftPf& pf
     pf.u = draw_uniform(P, b, i, 0, &ovr);   // perf mode: Philox, no stream words
 }
 __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out = nullptr,
-                           bool publish = true, bool coh = true);
+                           bool publish = true, bool coh = true, const uint32_t* poll_epoch = nullptr);
+
+// Poll-mode tag of k_stats' partial record (slot s, chunk c) of sequence b (k_draw_lean's protocol,
+// its own salt; the sequence's epoch lives in counter set 3, shared with k_sample's finish)
+__device__ __forceinline__ uint32_t stats_tag(uint32_t epoch, int b, int s, int c) {
+    uint32_t h = epoch * 0x9E3779B1u + (uint32_t)b * 0x85EBCA77u + (uint32_t)(s * 4096 + c) * 0xC2B2AE3Du + 0x3C6EF372u;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;   // murmur3 fmix32
+    return h | 1u;
+}
+__device__ __forceinline__ uint4* stats_rec(const Plan& P, int b, int s, int c) {
+    return reinterpret_cast<uint4*>(P.rpart) + ((int64_t)b * P.stat_slots + s) * P.n_chunks + c;
+}
 
 // Arrival at a per-sequence counter (thread 0, after storing its partials with st_coh): true for
 // the last of `total` arrivals, which also re-arms the counter.  coh_wait() completes the
@@ -350,6 +362,10 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     }
     const int r = b * P.slots + s;
     const void* row = slot_row(P, b, s);
+    // poll mode: this call's epoch of sequence b (thread 0, beside the first loads)
+    __shared__ uint32_t s_epoch;
+    if (TAIL && P.kpoll && threadIdx.x == 0)
+        s_epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // TAIL: drafted ids now (consumed after the loop), their logits right after it, so a
     // workgroup that turns out to be its sequence's last arrival has them in registers
     DraftPf pf;
@@ -471,20 +487,33 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     if (lane == 0) { lm[w] = m; ls[w] = acc; }
     __syncthreads();
     SD_TS(wg_id, 1);
+    // poll mode (TAIL): one tagged 16-byte record per (slot, span); the sequence's last span of its
+    // last slot (the ragged one) is the consumer: it polls the records and decides — no counter.
+    // Counter mode: the (m, S) partial and an arrival; the last arrival decides.
+    const bool poll = TAIL && P.kpoll;
     if (threadIdx.x == 0) {
         float M = lm[0], S = ls[0];
         for (int k = 1; k < kThreads / kWave; ++k) online_merge(M, S, lm[k], ls[k]);
-        st_coh(P.part + (int64_t)r * P.n_chunks + chunk, make_float2(M, S));
+        if (poll)
+            st_coh16(stats_rec(P, b, s, chunk), make_uint4(__float_as_uint(M), __float_as_uint(S),
+                                                           stats_tag(s_epoch, b, s, chunk), 0u));
+        else
+            st_coh(P.part + (int64_t)r * P.n_chunks + chunk, make_float2(M, S));
     }
     if constexpr (TAIL) {
         __shared__ int s_last;
-        if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.stat_slots * P.n_chunks));
-        __syncthreads();
-        SD_TS(wg_id, 2);
-        if (s_last) {
-            decide_seq(P, b, pf, wg_id);
-            SD_TS(wg_id, 3);
+        if (poll) {
+            if (s != P.stat_slots - 1 || chunk != P.n_chunks - 1) return;
+        } else {
+            if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.stat_slots * P.n_chunks));
+            __syncthreads();
+            SD_TS(wg_id, 2);
+            if (!s_last) return;
         }
+        decide_seq(P, b, pf, wg_id, nullptr, true, true, poll ? &s_epoch : nullptr);
+        SD_TS(wg_id, 3);
+        if (poll && threadIdx.x == 0)
+            __hip_atomic_store(seq_counter(P.cnt, 3, b), s_epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -756,7 +785,8 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
 // uniforms, the walk.  Every per-draft input was prefetched during the stream (DraftPf), so the
 // tail has one memory round trip (the partials).  With the drafter stats prefetched (P.dstats)
 // the wave that reduces target slot i tests draft i at once: one barrier before the walk.
-__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out, bool publish, bool coh) {
+__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out, bool publish, bool coh,
+                           const uint32_t* poll_epoch) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
     __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
     __shared__ uint8_t lacc[SD_MAX_GAMMA], lstop[SD_MAX_GAMMA];
@@ -770,11 +800,31 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, D
         }
         constexpr int kMaxSlotsPerWave = (SD_MAX_GAMMA + 1 + 3) / 4;
         float2 v[kMaxSlotsPerWave];
+        if (poll_epoch) {   // poll mode: each record re-read until it carries this call's tag (bounded)
+            const uint32_t ep = *poll_epoch;
 #pragma unroll
-        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
-            const int s = w + k * nw;
-            v[k] = (s < P.n_tslots && lane < P.n_chunks) ? ld_x(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane, coh)
-                                                         : make_float2(-INFINITY, 0.f);
+            for (int k = 0; k < kMaxSlotsPerWave; ++k) {
+                const int s = w + k * nw;
+                v[k] = make_float2(-INFINITY, 0.f);
+                if (s < P.n_tslots && lane < P.n_chunks) {
+                    const uint4* rp = stats_rec(P, b, s, lane);
+                    const uint32_t tag = stats_tag(ep, b, s, lane);
+                    uint4 r = ld_coh16(rp);
+                    for (int spin = 0; r.z != tag && spin < (1 << 16); ++spin) {
+                        __builtin_amdgcn_s_sleep(1);
+                        r = ld_coh16(rp);
+                    }
+                    v[k] = r.z == tag ? make_float2(__uint_as_float(r.x), __uint_as_float(r.y))
+                                      : make_float2(0.f, NAN);   // timeout: the row is flagged invalid
+                }
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < kMaxSlotsPerWave; ++k) {
+                const int s = w + k * nw;
+                v[k] = (s < P.n_tslots && lane < P.n_chunks) ? ld_x(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane, coh)
+                                                             : make_float2(-INFINITY, 0.f);
+            }
         }
 #pragma unroll
         for (int k = 0; k < kMaxSlotsPerWave; ++k) {
@@ -2450,11 +2500,19 @@ int32_t launch_stats(const sd::Plan& P, void* stream, bool tail = false);
 // errors left behind by earlier, unrelated runtime calls must not be blamed on our launches
 inline void clear_stale_error() { (void)hipGetLastError(); }
 
+bool sample_poll_ok(int B, const void* kern);
+
 template <int DT, bool TAIL>
 int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt, void* stream) {
     const dim3 grid(P.n_chunks, P.B * slot_cnt);
-    if (fast) SD_LAUNCH((k_stats<DT, true, TAIL>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
-    else SD_LAUNCH((k_stats<DT, false, TAIL>), grid, dim3(kThreads), stream, P, slot_lo, slot_cnt);
+    // poll-mode decide tail: the drafter stats came with the draws (target slots only, one launch)
+    sd::Plan Q = P;
+    static const bool kp_off = getenv("SD_STATS_POLL") && atoi(getenv("SD_STATS_POLL")) == 0;   // A/B
+    Q.kpoll = TAIL && !kp_off && P.dstats && P.n_chunks <= kWave && P.stat_slots == P.n_tslots && slot_lo == 0 &&
+              slot_cnt == P.stat_slots &&
+              sample_poll_ok(P.B, fast ? (const void*)k_stats<DT, true, TAIL> : (const void*)k_stats<DT, false, TAIL>);
+    if (fast) SD_LAUNCH((k_stats<DT, true, TAIL>), grid, dim3(kThreads), stream, Q, slot_lo, slot_cnt);
+    else SD_LAUNCH((k_stats<DT, false, TAIL>), grid, dim3(kThreads), stream, Q, slot_lo, slot_cnt);
     return SD_OK;
 }
 
@@ -2470,9 +2528,9 @@ int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, in
     return launch_stats_dt<SD_F16, false>(P, fast, slot_lo, slot_cnt, stream);
 }
 
-// k_sample's poll-mode finish needs its B consumers plus at least one producer resident: B < the
-// kernel's resident capacity (occupancy x CUs, per device and kernel, queried once); SD_SAMPLE_POLL=0
-// keeps the arrival counter (A/B)
+// A poll-mode exchange (k_sample's finish, k_stats' decide tail) needs its B consumers plus producers
+// resident: 2B <= the kernel's resident capacity (occupancy x CUs, per device and kernel, queried
+// once); SD_SAMPLE_POLL=0 keeps the arrival counters (A/B)
 bool sample_poll_ok(int B, const void* kern) {
     static const bool off = getenv("SD_SAMPLE_POLL") && atoi(getenv("SD_SAMPLE_POLL")) == 0;
     if (off) return false;
