@@ -58,6 +58,8 @@ def graph_time(step, steps=200, per_graph=20):
 
 
 def cpu_time(fn, seconds=3.0):
+    if os.environ.get("CFG_NO_CPU"):   # GPU-only A/B runs
+        return None
     torch.set_num_threads(CPU_THREADS)
     fn()
     n, t0 = 0, time.perf_counter()
