@@ -2466,10 +2466,11 @@ bool needs_keep(const sd_processor& p) { return p.kind >= SD_PROC_TOPK; }
 // fewer arrivals and partials per sequence for the decision tail, until the stream itself thins
 // out.  SD_STATS_STAGES overrides (tuning).
 // Other callers (sd_sample's greedy / STREAM statistics, A11) keep target_wgs = 2048.
-void set_stats_chunks(sd::Plan& P, int rows, int target_wgs = 2048) {
+void set_stats_chunks(sd::Plan& P, int rows, int target_wgs = 2048, int min_stages = 1) {
     const int64_t stage = kThreads * 8;
     const int64_t stages_per_row = (P.V + stage - 1) / stage;
     int64_t per_wg = (rows * stages_per_row + target_wgs - 1) / target_wgs;
+    per_wg = per_wg < min_stages ? min_stages : per_wg;
     if (const char* e = getenv("SD_STATS_STAGES")) per_wg = atoi(e);
     per_wg = per_wg < 1 ? 1 : (per_wg > 64 ? 64 : per_wg);
     P.chunk = (int32_t)(per_wg * stage);
@@ -2814,7 +2815,9 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         P.stat_slots = P.n_tslots;
     }
 
-    set_stats_chunks(P, P.B * P.stat_slots, 512);   // the rows k_stats streams
+    // the rows k_stats streams; at least 8 stages per workgroup: few rows (batch 1) then take 8 spans
+    // per row instead of 63 one-stage ones (configs[1] multinomial 36.1 -> 33.7 us per step)
+    set_stats_chunks(P, P.B * P.stat_slots, 512, 8);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->batch * (2 * a->gamma + 1), a->batch, a->gamma, a->vocab);
 
