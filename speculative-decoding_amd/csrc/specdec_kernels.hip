@@ -115,6 +115,7 @@ struct Plan {
     int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
     int32_t spoll;        // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
     int32_t kpoll;        // k_stats (decide tail): poll-mode partials (tagged records, no counter)
+    int32_t thr_poll;     // k_thr_hist: slice maxima exchanged in-launch (no k_thr_max launch)
     // sd_ngram_verify (sd_ngram.inc)
     struct NgPart* ngpart;
     int64_t* filler_ids;
