@@ -377,6 +377,9 @@ __device__ __forceinline__ float wave_sum(float v) {
 __device__ __forceinline__ int wave_min_i(int v) {
     return wave_reduce_i(v, INT_MAX, [](int a, int b) { return a < b ? a : b; });
 }
+__device__ __forceinline__ int wave_sum_i(int v) {
+    return wave_reduce_i(v, 0, [](int a, int b) { return a + b; });
+}
 __device__ __forceinline__ int wave_max_i(int v) {
     return wave_reduce_i(v, INT_MIN, [](int a, int b) { return a > b ? a : b; });
 }

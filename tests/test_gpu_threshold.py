@@ -2,7 +2,9 @@
 the exact-arithmetic oracle (utils/logits_processor.py:59-103 restated in oracle/specdec_ref.py,
 fp64 softmax, equal values kept lowest index first), through sd_probs.
 
-Covers every path of the three-launch design: one and many slices per row, a partial last slice,
+Every test runs on both designs: the in-launch exchanges of k_thr_hist (slice maxima, tie search
+and radix hand-over through polled records) and the separate k_thr_max / k_thr_tie launches.
+Covers every path: one and many slices per row, a partial last slice,
 unaligned rows (scalar loads), fp16 keys (top-k: the reference's -1e20 fill raises in fp16),
 cuts inside long runs of equal values (the sliced tie
 search), and the rows handed to the radix descent (top-k rank or nucleus crossing below the
@@ -22,6 +24,15 @@ pytestmark = pytest.mark.gpu
 def ops():
     from specdec_amd import ops
     return ops
+
+
+@pytest.fixture(autouse=True, params=["in-launch", "launches"])
+def thr_design(request, monkeypatch):
+    """The slice maxima, tie search and radix hand-over inside k_thr_hist (polled records, the
+    default when the grid is resident) or in k_thr_max / k_thr_tie launches of their own
+    (SD_THR_POLL=0); the library reads the switch on every call."""
+    monkeypatch.setenv("SD_THR_POLL", "1" if request.param == "in-launch" else "0")
+    return request.param
 
 
 def normal_rows(R, V, dtype, seed, scale=3.0):
