@@ -743,12 +743,43 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
 
 __global__ void __launch_bounds__(256) k_walk(Plan P) {
     if (P.noise.mode == SD_NOISE_STREAM) {
-        // the reference draws row after row from one generator: serial by construction
-        if (threadIdx.x == 0) {
-            int64_t off = 0;
-            for (int b = 0; b < P.B; ++b) off += walk_seq(P, b, off);
-            if (P.words_used) *P.words_used = off;
+        // The reference draws row after row from one generator: the rows' word offsets form a serial
+        // chain.  One wave walks it, each row in one round trip: lane i loads draft i's uniform (at
+        // the row's offset), its p/q and its drafted id together and tests it; lane 0 walks the
+        // flags (walk_core's rules) and moves the offset.
+        __shared__ uint8_t lacc[SD_MAX_GAMMA], lstop[SD_MAX_GAMMA];
+        if (threadIdx.x >= kWave) return;
+        const int lane = threadIdx.x, g = P.gamma;
+        int64_t off = 0;
+        for (int b = 0; b < P.B; ++b) {
+            bool acc = false, stop = false, ovr = false;
+            if (lane < g) {
+                const int64_t w = off + lane;
+                ovr = w >= P.noise.n_words;
+                const float u = ovr ? 0.f : uniform_from_word(P.noise.words[w]);
+                acc = accept_draft(P, P.rp[b * g + lane], P.rq[b * g + lane], u);
+                stop = is_stop(P, P.draft_tokens[b * P.tok_stride + lane]);
+            }
+            const uint64_t accm = __ballot(acc), stopm = __ballot(stop), ovrm = __ballot(ovr);
+            int64_t next = off;
+            if (lane == 0) {
+                for (int i = 0; i < g; ++i) {
+                    lacc[i] = (uint8_t)((accm >> i) & 1u);
+                    lstop[i] = (uint8_t)((stopm >> i) & 1u);
+                }
+                int64_t used;
+                Decision d = walk_core(P, b, P.rp + b * g, P.rq + b * g, off, &used, lacc, lstop);
+                // the uniforms come first in a row's words: SPEC reads all γ', ENGINE one per tested draft
+                const int64_t n_u = P.rule == SD_RULE_SPEC ? g : (d.mode == kModeResid ? used - 2ll * P.V : used);
+                const uint64_t umask = n_u >= 64 ? ~0ull : ((1ull << n_u) - 1ull);
+                if (ovrm & umask) d.status |= SD_ROW_NOISE_OVERRUN;
+                publish_decision(P, b, d);
+                next = off + used;
+            }
+            off = ((int64_t)__builtin_amdgcn_readlane((int)(next >> 32), 0) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)(next & 0xffffffff), 0);
         }
+        if (lane == 0 && P.words_used) *P.words_used = off;
     } else {
         for (int b = threadIdx.x; b < P.B; b += blockDim.x) walk_seq(P, b, 0);
         if (threadIdx.x == 0 && P.words_used) *P.words_used = 0;
