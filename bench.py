@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stream-steps", type=int, default=5, help="STREAM-mode (bit-exact noise) steps; 0 = skip")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] batch-1 lines")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL, one GPU per rank) or gloo (rehearsing N ranks on fewer GPUs)")
     return ap.parse_args()
 
 
@@ -183,12 +185,16 @@ def main():
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if not torch.cuda.is_available():
         raise SystemExit("bench.py needs a GPU")
+    local = local % torch.cuda.device_count()   # == local on a node with a GPU per rank
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import specdec_amd  # noqa: F401
     from specdec_amd import _lib, dp, ops
