@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 6
+#define SD_ABI_VERSION 7
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -108,6 +108,16 @@ typedef struct {
 #define SD_ROW_EXCHANGE_TIMEOUT 0x200 /* a workgroup's partial never arrived within the bounded
                                        wait of an in-launch exchange (k_draw_lean); the row's
                                        outputs are invalid (also flagged SD_ROW_INVALID_DIST)    */
+
+/* A top-k / nucleus row's keep predicate (the threshold search's result): token j is kept iff
+ * x_j > tau || (x_j == tau && j <= tie_idx), x_j the row's logit (tau = -inf, tie_idx = INT_MAX
+ * keeps all).  flags: SD_ROW_* bits the search raised (SD_ROW_NUCLEUS_INEXACT).  16 bytes.   */
+typedef struct sd_row_keep {
+    float tau;
+    int32_t tie_idx;
+    int32_t flags;
+    int32_t reserved;
+} sd_row_keep;
 
 typedef struct {
     /* shape */
@@ -183,6 +193,13 @@ typedef struct {
        top-k / nucleus drafter processor.                                                      */
     const float* draft_row_stats;
     int64_t draft_row_stats_stride;
+    /* optional (nullable, read only with draft_row_stats): the keep predicates of a top-k /
+       nucleus drafter's rows as sd_sample returned them with the draws (sd_sample_args.row_keep),
+       at draft_row_stats' layout: row d of sequence b at draft_row_keep[d * stride + b].  With
+       both, the drafter rows are neither re-read for their statistics nor re-searched for their
+       thresholds: the keep is a function of the row and draft_proc alone, so the draw's equals
+       the one the verify would compute (utils/logits_processor.py:52-101).                    */
+    const struct sd_row_keep* draft_row_keep;
 } sd_verify_args;
 
 typedef struct {
@@ -204,6 +221,9 @@ typedef struct {
                                     normaliser pair sd_verify takes as draft_row_stats (nullable).
                                     PHILOX stochastic rows: ONE pass (k_draw) — each span draws
                                     its own candidate, the row's last workgroup picks the span  */
+    struct sd_row_keep* row_keep; /* [R] keep predicate of each row under a top-k / nucleus
+                                    processor, the input sd_verify takes as draft_row_keep
+                                    (nullable; not written for other processors)               */
 } sd_sample_args;
 
 /* LogitsProcessor.__call__ (utils/logits_processor.py:13-15) materialised: probs = softmax(_process(l)/T)

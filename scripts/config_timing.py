@@ -90,10 +90,19 @@ def cfg1(kind, top_p=1.0):
     trows = [tl[:, t] for t in range(g + 1)]
     drows = [dl[:, t] for t in range(g)]
 
+    # the draws hand their rows' stats (and top-k / nucleus keeps) to the verify, as the drop-in
+    # loop does; CFG_NO_STASH=1: the verify recomputes them (A/B)
+    stash = not os.environ.get("CFG_NO_STASH")
+    dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev) if stash else None
+    dkeep = torch.empty(g, 1, 4, dtype=torch.int32, device=dev) if stash and proc.keeps else None
+
     def step():
         for d in range(g):
-            ops.sample_rows(drows[d], proc, noise, tokens_out=draft[:, d])
-        return ops.verify(trows, drows, draft, _lib.SD_RULE_SPEC, proc, proc, noise, STOPS)
+            ops.sample_rows(drows[d], proc, noise, tokens_out=draft[:, d],
+                            row_stats_out=dstats[d] if stash else None,
+                            row_keep_out=dkeep[d] if dkeep is not None else None)
+        return ops.verify(trows, drows, draft, _lib.SD_RULE_SPEC, proc, proc, noise, STOPS,
+                          draft_row_stats=dstats, draft_row_keep=dkeep)
 
     us = graph_time(step)
     # oracle: drafter process + sample per position, then the A8 verify step (torch-CPU)

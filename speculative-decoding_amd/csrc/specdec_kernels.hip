@@ -88,6 +88,8 @@ struct Plan {
     const float2* dstats;       // sd_verify: drafter row stats from sd_sample (nullable)
     int64_t dstats_stride;      // element (d, b) at dstats[d * dstats_stride + b]
     int32_t stat_slots;         // slots whose stats k_stats computes (the rest come from dstats)
+    const RowKeep* dkeep;       // sd_verify: drafter keep predicates from sd_sample, at dstats' layout (nullable)
+    RowKeep* keep_out;          // sd_sample: each row's keep predicate out (nullable)
     int64_t* generated;
     int64_t gen_stride;
     int32_t step;
@@ -161,6 +163,16 @@ __device__ __forceinline__ const void* row_ptr(const Plan& P, int r, int* dt, fl
     }
     *dt = P.ddt; *T = P.dT; *keep = P.d_keep;
     return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
+}
+
+// row r's keep predicate: the threshold search's, or for a drafter row whose draw returned it
+// (sd_verify_args.draft_row_keep) the draw's
+__device__ __forceinline__ RowKeep keep_of(const Plan& P, int r) {
+    if (P.dkeep) {
+        const int b = r / P.slots, s = r - b * P.slots;
+        if (s >= P.n_tslots) return P.dkeep[(int64_t)(s - P.n_tslots) * P.dstats_stride + b];
+    }
+    return P.keep[r];
 }
 
 __device__ __forceinline__ bool is_stop(const Plan& P, int64_t tok) {
@@ -375,7 +387,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     const bool is_t = s < P.n_tslots;
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
-    const RowKeep kp = has_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kp = has_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     // This workgroup's stages (STEP elements each) of the row: interleaved (stage chunk + i * n_chunks,
     // so concurrently running workgroups stream adjacent blocks) or one contiguous span.
     const int nst = (P.V + STEP - 1) / STEP;
@@ -613,7 +625,7 @@ __device__ void seq_ratios(const Plan& P, int b, const float2* lstat, float* lp,
     int dt; float T; bool keep;
     const int rt = b * P.slots + i;
     const void* trow = row_ptr(P, rt, &dt, &T, &keep);
-    const RowKeep kt = keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kt = keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     float p = 0.f, q = 0.f;
     if (tok >= 0 && tok < P.V) {
         p = prob_dyn(dt, trow, tok, T, keep, kt, lstat[i]);
@@ -622,7 +634,7 @@ __device__ void seq_ratios(const Plan& P, int b, const float2* lstat, float* lp,
         } else {
             const int rd = b * P.slots + P.n_tslots + i;
             const void* drow = row_ptr(P, rd, &dt, &T, &keep);
-            const RowKeep kd = keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+            const RowKeep kd = keep ? keep_of(P, rd) : RowKeep{-INFINITY, INT_MAX, 0, 0};
             q = prob_dyn(dt, drow, tok, T, keep, kd, lstat[P.n_tslots + i]);
         }
     }
@@ -793,7 +805,7 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
     q = 0.f;
     if (pf.tok < 0 || pf.tok >= P.V) return;
     const int rt = b * P.slots + i;
-    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const float yt = P.tdt == SD_BF16 ? process_value<SD_BF16>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
                    : P.tdt == SD_F32 ? process_value<SD_F32>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
                                      : process_value<SD_F16>(pf.xt, pf.tok, P.tT, P.t_keep, kt);
@@ -803,7 +815,7 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
         return;
     }
     const int rd = b * P.slots + P.n_tslots + i;
-    const RowKeep kd = P.d_keep ? P.keep[rd] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kd = P.d_keep ? keep_of(P, rd) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const float yd = P.ddt == SD_BF16 ? process_value<SD_BF16>(pf.xd, pf.tok, P.dT, P.d_keep, kd)
                    : P.ddt == SD_F32 ? process_value<SD_F32>(pf.xd, pf.tok, P.dT, P.d_keep, kd)
                                      : process_value<SD_F16>(pf.xd, pf.tok, P.dT, P.d_keep, kd);
@@ -976,7 +988,7 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
     const int rt = b * P.slots + d.slot;
     const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
     const bool t_al = (reinterpret_cast<uintptr_t>(trow) & 15) == 0;
-    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const bool stoch = P.t_stoch != 0;
     const int64_t base = (int64_t)c * P.rchunk;
     const void* drow;
@@ -987,7 +999,7 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
     } else {
         const int rd = b * P.slots + P.n_tslots + d.slot;
         drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
-        if (P.d_keep) kd = P.keep[rd];
+        if (P.d_keep) kd = keep_of(P, rd);
     }
     const bool d_al = (reinterpret_cast<uintptr_t>(drow) & 15) == 0;
     const float t_inv = 1.0f / mst.y, d_inv = 1.0f / msd.y;
@@ -1066,7 +1078,7 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
     const int rt = b * P.slots + d.slot;
     const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
     const bool t_al = (reinterpret_cast<uintptr_t>(trow) & 15) == 0;
-    const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const bool stoch = P.t_stoch != 0;
     const int64_t base = (int64_t)c * P.rchunk;
     const float t_inv = 1.0f / mst.y;
@@ -1139,7 +1151,7 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
         const float s = resid_mass(P, b, &wm);
         mass = s;
         const int rt = b * P.slots + d.slot;
-        const RowKeep kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+        const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
         const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
         const float2 mst = P.rowstat[rt];
         if (P.rule == SD_RULE_ENGINE && (double)s <= 1e-12) {
@@ -1187,7 +1199,7 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
                 else {
                     const int rd = b * P.slots + P.n_tslots + d.slot;
                     drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
-                    if (P.d_keep) kd = P.keep[rd];
+                    if (P.d_keep) kd = keep_of(P, rd);
                     msd = P.rowstat[rd];
                     ddt = P.ddt;
                 }
@@ -1241,9 +1253,9 @@ __device__ void finalize_write(const Plan& P, int b, const Decision& d, int64_t 
         status |= SD_ROW_FINISHED;
     }
     if (P.t_keep)
-        for (int s2 = 0; s2 < P.n_tslots; ++s2) status |= P.keep[b * P.slots + s2].flags;
+        for (int s2 = 0; s2 < P.n_tslots; ++s2) status |= keep_of(P, b * P.slots + s2).flags;
     if (P.d_keep)
-        for (int s2 = P.n_tslots; s2 < P.slots; ++s2) status |= P.keep[b * P.slots + s2].flags;
+        for (int s2 = P.n_tslots; s2 < P.slots; ++s2) status |= keep_of(P, b * P.slots + s2).flags;
     P.row_status[b] = status;
 }
 
@@ -1281,7 +1293,7 @@ __device__ __forceinline__ PairRows pair_rows(const Plan& P, const Decision& d, 
     R.resid = d.mode == kModeResid;
     const int rt = b * P.slots + d.slot;
     R.trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (TDT == SD_F32 ? 4 : 2);
-    R.kt = P.t_keep ? P.keep[rt] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    R.kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     R.kd = RowKeep{-INFINITY, INT_MAX, 0, 0};
     R.mst = d.mst;   // perf mode: carried by the decision (no dependent rowstat load)
     R.msd = make_float2(0.f, 1.f);
@@ -1292,7 +1304,7 @@ __device__ __forceinline__ PairRows pair_rows(const Plan& P, const Decision& d, 
         } else {
             const int rd = b * P.slots + P.n_tslots + d.slot;
             R.drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (DDT == SD_F32 ? 4 : 2);
-            if (P.d_keep) R.kd = P.keep[rd];
+            if (P.d_keep) R.kd = keep_of(P, rd);
             R.msd = d.msd;
         }
     }
@@ -1731,7 +1743,7 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
     const float2 ms = lms;
     const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-    const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kp = P.t_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const int64_t base = (int64_t)c * P.rchunk;
     const int64_t woff = 2ll * P.V * r;
     const float inv_s = 1.0f / ms.y;
@@ -1781,17 +1793,18 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
     if (lane == 0) {
         int32_t st = SD_ROW_DONE;
         if (P.t_stoch && (!(ms.y > 0.f) || ms.y != ms.y)) st |= SD_ROW_INVALID_DIST;
-        if (P.t_keep) st |= P.keep[r].flags;
+        if (P.t_keep) st |= keep_of(P, r).flags;
         if (P.noise.mode == SD_NOISE_STREAM && P.t_stoch && 2ll * P.V * P.B > P.noise.n_words)
             st |= SD_ROW_NOISE_OVERRUN;
         P.next_token[r * P.next_token_stride] = pi;
         if (P.token_prob) {
             const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
-            const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+            const RowKeep kp = P.t_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
             P.token_prob[r] = (pi >= 0 && pi < P.V) ? prob_dyn(P.tdt, row, pi, P.tT, P.t_keep, kp, ms) : NAN;
         }
         if (P.row_stats) P.row_stats[r] = ms;
         if (P.row_status) P.row_status[r] = st;
+        if (P.keep_out && P.t_keep) P.keep_out[r] = keep_of(P, r);
         if (r == 0 && P.words_used) *P.words_used = P.t_stoch ? 2ll * P.V * P.B : 0;
     }
 }
@@ -1817,7 +1830,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     else { r = blockIdx.y; c = blockIdx.x; }
     const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-    const RowKeep kp = (!FAST && P.t_keep) ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kp = (!FAST && P.t_keep) ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const int64_t base = (int64_t)c * NST * STEP;
     // The Philox uniforms run on the scalar unit, which every wave of the CU shares: computed by
     // each wave ahead of its loads (as the compiler scheduled them) they held back the launch's
@@ -1996,13 +2009,14 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
     if (threadIdx.x == 0) {
         int32_t st = SD_ROW_DONE;
         if (!(ms.y > 0.f) || ms.y != ms.y || ms.y == INFINITY) st |= SD_ROW_INVALID_DIST;   // torch raises
-        if (P.t_keep) st |= P.keep[r].flags;
+        if (P.t_keep) st |= keep_of(P, r).flags;
         const int64_t x = cp >= 0 ? (int64_t)l_cand[cp] : -1;
         if (x < 0) st |= SD_ROW_INVALID_DIST;
         P.next_token[r * P.next_token_stride] = x;
         if (P.token_prob) P.token_prob[r] = x >= 0 ? prob_exact<DT>(l_y[cp], ms.x, ms.y, 1.0f / ms.y) : NAN;
         if (P.row_stats) P.row_stats[r] = ms;
         if (P.row_status) P.row_status[r] = st;
+        if (P.keep_out && P.t_keep) P.keep_out[r] = keep_of(P, r);
         if (r == 0 && P.words_used) *P.words_used = 0;
     }
     SD_TS(wg_id, 6);
@@ -2409,7 +2423,7 @@ __device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r
     const float2 ms = lms;
     const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
     const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
-    const RowKeep kp = P.t_keep ? P.keep[r] : RowKeep{-INFINITY, INT_MAX, 0, 0};
+    const RowKeep kp = P.t_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const int64_t base = (int64_t)c * P.rchunk;
     char* orow = static_cast<char*>(out) + r * ostride * (DT == SD_F32 ? 4 : 2);
 #pragma unroll
@@ -2839,12 +2853,15 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.generated = a->generated; P.gen_stride = a->generated_stride_b; P.step = a->step;
     P.finished = a->finished; P.accepted_count = a->accepted_count;
     // drafter row stats that came with the draws (sd_sample row_stats): k_stats reads only the
-    // target rows.  A hint: ignored where the drafter rows carry a top-k / nucleus mask.
-    if (a->draft_row_stats && !a->draft_is_probs && !P.d_keep) {
+    // target rows.  A top-k / nucleus drafter also needs the draws' keep predicates
+    // (sd_sample row_keep): then the threshold search covers the target rows only.  Without
+    // them the stats are a hint the call ignores.
+    if (a->draft_row_stats && !a->draft_is_probs && (!P.d_keep || a->draft_row_keep)) {
         if (a->draft_row_stats_stride < a->batch) return SD_ERR_INVALID;
         P.dstats = reinterpret_cast<const float2*>(a->draft_row_stats);
         P.dstats_stride = a->draft_row_stats_stride;
         P.stat_slots = P.n_tslots;
+        if (P.d_keep) P.dkeep = reinterpret_cast<const RowKeep*>(a->draft_row_keep);
     }
 
     // the rows k_stats streams; at least 8 stages per workgroup: few rows (batch 1) then take 8 spans
@@ -2853,8 +2870,10 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->batch * (2 * a->gamma + 1), a->batch, a->gamma, a->vocab);
 
-    if (P.t_keep || P.d_keep) {
-        const int32_t st = launch_threshold(P, a->target_proc, a->draft_proc, stream);
+    if (P.t_keep || (P.d_keep && !P.dkeep)) {
+        Plan Q = P;                  // the drafter rows' keeps came with their draws: skip them
+        if (P.dkeep) Q.d_keep = 0;
+        const int32_t st = launch_threshold(Q, a->target_proc, a->draft_proc, stream);
         if (st != SD_OK) return st;
     }
     set_rchunks(P);
@@ -2913,6 +2932,7 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     P.next_token = a->tokens; P.next_token_stride = a->tokens_stride;
     P.token_prob = a->token_prob; P.row_status = a->row_status; P.words_used = a->words_used;
     P.row_stats = reinterpret_cast<float2*>(a->row_stats);
+    P.keep_out = reinterpret_cast<RowKeep*>(a->row_keep);
     set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);

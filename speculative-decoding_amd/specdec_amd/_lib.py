@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 6
+SD_ABI_VERSION = 7
 SD_MAX_GAMMA = 16
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
@@ -98,6 +98,7 @@ class sd_verify_args(C.Structure):
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
         ("prof_stats_begin", C.c_void_p), ("prof_stats_end", C.c_void_p), ("prof_stats_repeat", C.c_int32),
         ("draft_row_stats", C.c_void_p), ("draft_row_stats_stride", C.c_int64),
+        ("draft_row_keep", C.c_void_p),
     ]
 
 
@@ -108,7 +109,7 @@ class sd_sample_args(C.Structure):
         ("tokens", C.c_void_p), ("tokens_stride", C.c_int64), ("token_prob", C.c_void_p),
         ("row_status", C.c_void_p), ("words_used", C.c_void_p),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
-        ("row_stats", C.c_void_p),
+        ("row_stats", C.c_void_p), ("row_keep", C.c_void_p),
     ]
 
 

@@ -37,6 +37,11 @@ class ProcSpec:
     def stochastic(self) -> bool:
         return self.kind != "greedy"
 
+    @property
+    def keeps(self) -> bool:
+        """top-k / nucleus: rows carry a keep predicate (sd_row_keep)"""
+        return KIND[self.kind] >= _lib.SD_PROC_TOPK
+
     def struct(self) -> _lib.sd_processor:
         return _lib.sd_processor(KIND[self.kind], float(self.temperature), int(self.top_k), float(self.top_p))
 
@@ -123,7 +128,8 @@ def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
 
 # --------------------------------------------------------------------------- sampling
 def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Tensor] = None,
-                want_prob: bool = False, row_base: int = 0, row_stats_out: Optional[torch.Tensor] = None):
+                want_prob: bool = False, row_base: int = 0, row_stats_out: Optional[torch.Tensor] = None,
+                row_keep_out: Optional[torch.Tensor] = None):
     """LogitsProcessor.__call__ + .sample on every row of logits [R, V] (one sample per row).
 
     Returns (tokens int64 [R], token_prob fp32 [R] or None, row_status int32 [R]).  Under
@@ -131,6 +137,10 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     row_stats_out: optional fp32 [R, 2] device tensor (contiguous) that receives each processed
     row's (max, Σexp) — what ``verify(draft_row_stats=...)`` takes so the verify step does not
     re-read the drafter rows.  Under PhiloxNoise stochastic rows are drawn in ONE pass (k_draw).
+    row_keep_out: optional int32 [R, 4] contiguous device tensor that receives a top-k / nucleus
+    row's keep predicate (sd_row_keep: tau as fp32 bits, tie index, flags) — what
+    ``verify(draft_row_keep=...)`` takes with the stats so the verify skips the drafter rows'
+    threshold search.  Not written for other processors.
     """
     spec = proc_spec(proc)
     R, V = logits.shape
@@ -144,6 +154,9 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     if row_stats_out is not None and (row_stats_out.dtype != torch.float32 or not row_stats_out.is_cuda
                                       or row_stats_out.numel() < 2 * R or not row_stats_out.is_contiguous()):
         raise ValueError("row_stats_out must be a contiguous fp32 device tensor with >= 2*rows elements")
+    if row_keep_out is not None and (row_keep_out.dtype != torch.int32 or not row_keep_out.is_cuda
+                                     or row_keep_out.numel() < 4 * R or not row_keep_out.is_contiguous()):
+        raise ValueError("row_keep_out must be a contiguous int32 device tensor with >= 4*rows elements")
     need = 2 * R * V if spec.stochastic else 0
     nz, keep = _noise_struct(noise, need, dev, row_base)
     nbytes = lib.sd_sample_workspace_size(R, V)
@@ -152,7 +165,8 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
                             tokens.data_ptr(), tokens.stride(0) if tokens.dim() == 1 else 1,
                             prob.data_ptr() if prob is not None else None, status.data_ptr(), None,
                             ws.data_ptr(), ws.numel(),
-                            row_stats_out.data_ptr() if row_stats_out is not None else None)
+                            row_stats_out.data_ptr() if row_stats_out is not None else None,
+                            row_keep_out.data_ptr() if row_keep_out is not None else None)
     _lib.check(lib.sd_sample(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_sample")
     if isinstance(noise, StreamNoise):
         noise.consumed(count=need)
@@ -195,7 +209,8 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
            skip_sample_adjustment: bool = False, draft_is_probs: bool = False,
            active: Optional[torch.Tensor] = None, engine_state: Optional[dict] = None,
            sync_noise: bool = True, prof_events=None, row_base: int = 0,
-           draft_row_stats: Optional[torch.Tensor] = None) -> VerifyOut:
+           draft_row_stats: Optional[torch.Tensor] = None,
+           draft_row_keep: Optional[torch.Tensor] = None) -> VerifyOut:
     """One verify step for B sequences.
 
     target_rows: γ+1 (SPEC) or γ (ENGINE) tensors [B, V] — row t of every sequence;
@@ -206,7 +221,11 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
     what one call over the whole batch would draw for the same rows).
     draft_row_stats: optional fp32 [γ, B, 2] (or [γ, S>=B, 2]) device tensor — the drafter rows'
     (max, Σexp) as ``sample_rows(row_stats_out=...)`` returned them with the draws; the
-    row-statistics pass then reads only the target rows.
+    row-statistics pass then reads only the target rows.  Ignored for a top-k / nucleus drafter
+    unless draft_row_keep comes with it.
+    draft_row_keep: optional int32 [γ, S, 4] device tensor at draft_row_stats' row layout — the
+    drafter rows' keep predicates as ``sample_rows(row_keep_out=...)`` returned them; the
+    threshold search then covers the target rows only.
     """
     gamma = len(draft_rows)
     if not 1 <= gamma <= _lib.SD_MAX_GAMMA:
@@ -245,6 +264,13 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         if ds.dtype != torch.float32 or ds.dim() != 3 or ds.shape[0] < gamma or ds.shape[1] < B \
                 or ds.shape[2] != 2 or ds.stride(2) != 1 or ds.stride(1) != 2 or ds.device != dev:
             raise ValueError(f"draft_row_stats must be fp32 [>={gamma}, >={B}, 2] with (max, sum) pairs on {dev}")
+    if draft_row_keep is not None:
+        dk = draft_row_keep
+        if draft_row_stats is None or dk.dtype != torch.int32 or dk.dim() != 3 or dk.shape[0] < gamma \
+                or dk.shape[1] < B or dk.shape[2] != 4 or dk.stride(2) != 1 or dk.stride(1) != 4 \
+                or dk.stride(0) // 4 != draft_row_stats.stride(0) // 2 or dk.device != dev:
+            raise ValueError("draft_row_keep must be int32 [>=gamma, >=B, 4] at draft_row_stats' row stride, "
+                             "and comes with draft_row_stats")
 
     i32 = dict(dtype=torch.int32, device=dev)
     # every output is written by the kernels (no fill launches)
@@ -290,6 +316,8 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
     if draft_row_stats is not None:
         a.draft_row_stats, a.draft_row_stats_stride = draft_row_stats.data_ptr(), draft_row_stats.stride(0) // 2
+    if draft_row_keep is not None:
+        a.draft_row_keep = draft_row_keep.data_ptr()
     if prof_events is not None:   # (torch.cuda.Event, torch.cuda.Event[, repeats]) around the row-stats kernel
         a.prof_stats_begin, a.prof_stats_end = prof_events[0].cuda_event, prof_events[1].cuda_event
         a.prof_stats_repeat = int(prof_events[2]) if len(prof_events) > 2 else 1

@@ -8,6 +8,7 @@ the verify step that takes the draws' row statistics instead of re-reading the d
 * verify(draft_row_stats=...) must decide as the host walk on the exact p/q does, and agree with
   the call that computes the drafter statistics itself.
 """
+import dataclasses
 from types import SimpleNamespace
 
 import numpy as np
@@ -239,3 +240,74 @@ def test_verify_with_draw_stats(sd, rule):
             u = [float(ph.accept_uniform(11, off, s, i)) for i in range(g)]
             bad += _walk_engine(p, q, u, ih[s], []) != int(na[s])
         assert bad <= 1
+
+
+def kept_count(x, keep):
+    """tokens a row's sd_row_keep keeps: x_j > tau or (x_j == tau and j <= tie_idx)"""
+    tau = keep[0:1].view(torch.float32)
+    tie = int(keep[1])
+    xf = x.float()
+    j = torch.arange(x.numel())
+    return int(((xf > tau) | ((xf == tau) & (j <= tie))).sum())
+
+
+@pytest.mark.parametrize("proc", [ref.Processor("nucleus", 1.0, 0, 0.9), ref.Processor("topk", 0.8, 50),
+                                  ref.Processor("topknucleus", 1.0, 200, 0.8)], ids=lambda p: p.kind)
+@pytest.mark.parametrize("dtype,V", [(torch.bfloat16, 128256), (torch.float16, 32000)])
+def test_verify_with_draw_keeps(sd, proc, dtype, V):
+    """A top-k / nucleus drafter: each draw also returns its row's keep predicate
+    (sample_rows(row_keep_out=...)), and verify(draft_row_stats, draft_row_keep) searches the
+    thresholds of the target rows only.  The keeps count what the oracle's processor keeps
+    (utils/logits_processor.py:52-101), the same rows drawn again return the same keeps, and the
+    decisions equal the verify that recomputes everything but where the accept uniform sits
+    within fp32 rounding of p/q (the drafter's Σexp summed in another order)."""
+    import philox_ref as ph
+    B, g = 4, 4
+    tl = rand_logits((B, g + 1, V), dtype, 81).to(DEV)
+    dl = (tl[:, :g].float() + rand_logits((B, g, V), torch.float32, 82, 1.0).to(DEV)).to(dtype)
+    spec = spec_of(sd, proc)
+    noise = sd.PhiloxNoise(seed=13)
+    stats = torch.empty(g, B, 2, dtype=torch.float32, device=DEV)
+    keeps = torch.empty(g, B, 4, dtype=torch.int32, device=DEV)
+    ids = torch.empty(B, g, dtype=torch.long, device=DEV)
+    for d in range(g):
+        tok, _, _ = sd.ops.sample_rows(dl[:, d], spec, noise, row_stats_out=stats[d], row_keep_out=keeps[d])
+        ids[:, d] = tok
+    again = torch.empty_like(keeps[0])
+    sd.ops.sample_rows(dl[:, 1], spec, sd.PhiloxNoise(seed=99), row_keep_out=again)
+    assert torch.equal(again, keeps[1])
+    kc, dlc = keeps.cpu(), dl.cpu()
+    exact = dataclasses.replace(proc, stable_ties=True)   # the cut in exact arithmetic (test_gpu_threshold)
+    # fp16 rows: the reference cannot fill -1e20 into fp16 (torch raises); top-k ranks values only,
+    # so its count is checked on the same values in fp32, the nucleus cut has no fp16 reference
+    orows = dlc.float() if dtype == torch.float16 else dlc
+    for d in range(g if dtype != torch.float16 or proc.kind == "topk" else 0):
+        want = (ref.processed_logits(orows[:, d], exact, exact=True).float() > -1e19).sum(-1)
+        for b in range(B):
+            if not int(kc[d, b, 2]) & sd.lib.SD_ROW_NUCLEUS_INEXACT:
+                assert kept_count(dlc[b, d], kc[d, b]) == int(want[b]), (d, b)
+    trows = [tl[:, t] for t in range(g + 1)]
+    drows = [dl[:, d] for d in range(g)]
+    off = noise.offset
+    r = sd.lib.SD_RULE_SPEC
+    a = sd.ops.verify(trows, drows, ids, r, spec, spec, sd.PhiloxNoise(seed=13, offset=off), draft_row_stats=stats,
+                      draft_row_keep=keeps)
+    b = sd.ops.verify(trows, drows, ids, r, spec, spec, sd.PhiloxNoise(seed=13, offset=off))
+    assert torch.equal(a.row_status.cpu() & 0x1, b.row_status.cpu() & 0x1)
+    na, nb = a.n_accepted.cpu(), b.n_accepted.cpu()
+    same = na == nb
+    assert torch.equal(a.next_token.cpu()[same], b.next_token.cpu()[same])
+    tlc = tl[:, :g].cpu()
+    pp = ref.process(tlc.float() if dtype == torch.float16 else tlc, proc, exact=True).double()
+    qq = ref.process(orows, proc, exact=True).double()
+    tol = 1e-5 if dtype != torch.float16 else 2e-3     # fp16: p/q of the fp32-processed rows
+    ih = ids.cpu()
+    for s in (~same).nonzero().flatten().tolist():
+        i = min(int(na[s]), int(nb[s]))
+        p_i, q_i = float(pp[s, i, ih[s, i]]), float(qq[s, i, ih[s, i]])
+        ratio = min(1.0, p_i / q_i) if q_i > 0 else 1.0
+        u = float(ph.accept_uniform(13, off, s, i))
+        assert abs(u - ratio) <= tol * ratio + 1e-7, (s, i, u, ratio)
+        DRAW_CLOSE_CALLS.append(f"keep {proc.kind} row={s} draft={i} p/q={ratio:.9g} u={u:.9g}")
+    with pytest.raises(ValueError):   # keeps come with the stats
+        sd.ops.verify(trows, drows, ids, r, spec, spec, sd.PhiloxNoise(seed=13), draft_row_keep=keeps)

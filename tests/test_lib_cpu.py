@@ -39,6 +39,7 @@ int main(void) {
   printf("sd_sample_args %zu\n", sizeof(sd_sample_args));
   printf("sd_probs_args %zu\n", sizeof(sd_probs_args));
   printf("sd_noise %zu\n", sizeof(sd_noise));
+  printf("sd_row_keep %zu\n", sizeof(sd_row_keep));
   printf("sd_ngram_args %zu\n", sizeof(sd_ngram_args));
   printf("sd_ngram_store %zu\n", sizeof(sd_ngram_store));
   F(sd_ngram_store, gram_capacity) F(sd_ngram_store, pair_keys) F(sd_ngram_store, pair_capacity)
@@ -46,8 +47,8 @@ int main(void) {
   F(sd_verify_args, draft_rows) F(sd_verify_args, draft_tokens) F(sd_verify_args, target_proc)
   F(sd_verify_args, noise) F(sd_verify_args, n_accepted) F(sd_verify_args, generated)
   F(sd_verify_args, step) F(sd_verify_args, workspace_bytes) F(sd_verify_args, prof_stats_end) F(sd_verify_args, prof_stats_repeat)
-  F(sd_verify_args, draft_row_stats) F(sd_verify_args, draft_row_stats_stride)
-  F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes) F(sd_sample_args, row_stats)
+  F(sd_verify_args, draft_row_stats) F(sd_verify_args, draft_row_stats_stride) F(sd_verify_args, draft_row_keep)
+  F(sd_sample_args, noise) F(sd_sample_args, tokens) F(sd_sample_args, workspace_bytes) F(sd_sample_args, row_stats) F(sd_sample_args, row_keep)
   F(sd_probs_args, probs) F(sd_probs_args, workspace_bytes) F(sd_noise, row_base)
   F(sd_ngram_args, target_rows) F(sd_ngram_args, draft_tokens) F(sd_ngram_args, proc) F(sd_ngram_args, noise)
   F(sd_ngram_args, filler_ids) F(sd_ngram_args, workspace_bytes)
