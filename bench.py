@@ -371,15 +371,16 @@ def configs1_lines(dev, args, ops, _lib, PhiloxNoise):
                        ("nucleus_p0.9", ops.ProcSpec("nucleus", 1.0, 0, 0.9))):
         noise = PhiloxNoise(seed=7, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
         draft = torch.zeros(1, g, dtype=torch.long, device=dev)
-        dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev)
-        dkeep = torch.empty(g, 1, 4, dtype=torch.int32, device=dev) if proc.keeps else None
+        # as the drop-in loop does: the draws hand their rows' stats to the verify, except under a
+        # top-k / nucleus processor (the nucleus draw runs without a threshold search: k_draw_nuc)
+        dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev) if not proc.keeps else None
 
-        def step():   # the draws hand their rows' stats (and keeps) to the verify, as the drop-in loop does
+        def step():
             for d in range(g):
-                ops.sample_rows(drows[d], proc, noise, tokens_out=draft[:, d], row_stats_out=dstats[d],
-                                row_keep_out=dkeep[d] if dkeep is not None else None)
+                ops.sample_rows(drows[d], proc, noise, tokens_out=draft[:, d],
+                                row_stats_out=dstats[d] if dstats is not None else None)
             return ops.verify(trows, drows, draft, _lib.SD_RULE_SPEC, proc, proc, noise, stops,
-                              draft_row_stats=dstats, draft_row_keep=dkeep)
+                              draft_row_stats=dstats)
 
         for _ in range(5):
             step()

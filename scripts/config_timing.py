@@ -90,9 +90,10 @@ def cfg1(kind, top_p=1.0):
     trows = [tl[:, t] for t in range(g + 1)]
     drows = [dl[:, t] for t in range(g)]
 
-    # the draws hand their rows' stats (and top-k / nucleus keeps) to the verify, as the drop-in
-    # loop does; CFG_NO_STASH=1: the verify recomputes them (A/B)
-    stash = not os.environ.get("CFG_NO_STASH")
+    # as the drop-in loop does: the draws hand their rows' stats to the verify, except under a
+    # top-k / nucleus processor; CFG_KEEP_STASH=1: those draws return stats and keeps too (the
+    # threshold + k_draw path instead of k_draw_nuc), CFG_NO_STASH=1: no stats at all (A/B)
+    stash = not os.environ.get("CFG_NO_STASH") and (not proc.keeps or os.environ.get("CFG_KEEP_STASH"))
     dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev) if stash else None
     dkeep = torch.empty(g, 1, 4, dtype=torch.int32, device=dev) if stash and proc.keeps else None
 

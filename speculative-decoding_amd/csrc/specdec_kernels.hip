@@ -2456,6 +2456,7 @@ thread_local hipError_t g_last_error = hipSuccess;
 }  // namespace
 
 #include "sd_threshold.inc"
+#include "sd_draw_nucleus.inc"
 
 namespace {
 
@@ -2780,6 +2781,56 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
     return launch_draw_dt<SD_F16>(P, nst, stream);
 }
 
+// The nucleus drafter draw by rejection (k_draw_nuc, sd_draw_nucleus.inc) in place of the threshold
+// search + k_draw: PHILOX plain nucleus with top_p >= kNucMinP and T <= 1 (the proposal then keeps
+// >= top_p of its mass on the nucleus), 16-bit rows, no token_prob / row_stats / row_keep asked
+// (they need the nucleus' own normaliser), and the whole grid resident (its slices poll each other).
+// 1: launched; 0: not applicable.  SD_NUC_REJECT=0 turns it off (A/B, tests).
+int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* stream) {
+    if (P.noise.mode != SD_NOISE_PHILOX || proc.kind != SD_PROC_NUCLEUS) return 0;
+    if (!(proc.top_p >= sd::kNucMinP) || !(proc.temperature <= 1.f) || P.tdt == SD_F32) return 0;
+    if (P.token_prob || P.row_stats || P.keep_out) return 0;
+    if (const char* e = getenv("SD_NUC_REJECT"))
+        if (!atoi(e)) return 0;
+    const int nsl = (P.V + sd::kThrSlice - 1) / sd::kThrSlice;
+    if (nsl > kWave || P.B > kCntMax) return 0;
+    // the records (kNucRecs x 16 B per slice) inside the row's share of the ResPart region
+    if ((int64_t)nsl * sd::kNucRecs * 16 > (int64_t)(max_chunks(P.V) + 1) * (int64_t)sizeof(sd::ResPart)) return 0;
+    static int cap[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cap[dev] == 0) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sd::k_draw_nuc<SD_BF16>, sd::kThrThreads, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = cus = 0;
+        cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
+    }
+    if (cap[dev] <= 0 || (int64_t)nsl * P.B > cap[dev]) return 0;
+    sd::NucArgs A{};
+    A.rows = static_cast<const char*>(P.trow[0]);
+    A.stride_bytes = P.tstride * 2;
+    A.cnt = P.cnt;
+    A.rpart = reinterpret_cast<uint4*>(P.rpart);
+    A.next_token = P.next_token;
+    A.nt_stride = P.next_token_stride;
+    A.row_status = P.row_status;
+    A.words_used = P.words_used;
+    A.ts = P.ts;
+    A.noise = P.noise;
+    A.V = P.V;
+    A.T = proc.temperature;
+    A.top_p = proc.top_p;
+    const dim3 grid(nsl, P.B);
+    if (P.tdt == SD_BF16)
+        hipLaunchKernelGGL(sd::k_draw_nuc<SD_BF16>, grid, dim3(sd::kThrThreads), 0, (hipStream_t)stream, A);
+    else
+        hipLaunchKernelGGL(sd::k_draw_nuc<SD_F16>, grid, dim3(sd::kThrThreads), 0, (hipStream_t)stream, A);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) { g_last_error = e; return SD_ERR_LAUNCH; }
+    return 1;
+}
+
 }  // namespace
 
 extern "C" {
@@ -2939,6 +2990,7 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
 #ifdef SD_PHASE_TIMING
     if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
 #endif
+    if (const int32_t st = launch_draw_nuc(P, a->proc, stream)) return st < 0 ? st : SD_OK;
     if (P.t_keep) {
         const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
         if (st != SD_OK) return st;

@@ -125,11 +125,12 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         if t in stops:
             return input_ids[0, prompt_len:cur].tolist(), 0
 
-    # perf mode: each draw also returns its row's (max, Σexp) and, for a top-k / nucleus
-    # processor, its keep predicate, so verify reads and thresholds only the target rows
-    stash = isinstance(noise, PhiloxNoise) and torch.device(drafter.device) == torch.device(dev)
+    # perf mode: each draw also returns its row's (max, Σexp), so verify reads only target rows.
+    # Not for top-k / nucleus processors: their stats would need the draw's threshold search,
+    # which the nucleus draw skips (k_draw_nuc, rejection against the nucleus); the verify
+    # thresholds all its rows in one launch anyway.
+    stash = isinstance(noise, PhiloxNoise) and torch.device(drafter.device) == torch.device(dev) and not spec.keeps
     dstats = torch.empty(max(gamma, 1), 1, 2, dtype=torch.float32, device=dev) if stash else None
-    dkeep = torch.empty(max(gamma, 1), 1, 4, dtype=torch.int32, device=dev) if stash and spec.keeps else None
     while cur < total_len:                                       # :105
         g = min(gamma, total_len - cur - 1)                      # :106
         ids_d = input_ids.to(drafter.device)
@@ -140,8 +141,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
             dlen = cur + k
             row = logits[:, -1, :]
             sample_rows(row, spec, noise, tokens_out=ids_d[0, cur + k:cur + k + 1],
-                        row_stats_out=dstats[k] if stash else None,
-                        row_keep_out=dkeep[k] if dkeep is not None else None)
+                        row_stats_out=dstats[k] if stash else None)
             draft_rows.append(row if row.device == torch.device(dev) else row.to(dev))
         drafts_speculated += g
         input_ids = ids_d.to(dev)
@@ -159,8 +159,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         trows = [logits[:, cur - 1 + t - start, :] for t in range(g + 1)]   # :135 and bonus row :159
         out = verify(trows, draft_rows, input_ids[:, cur:cur + g], _lib.SD_RULE_SPEC, spec, spec, noise,
                      stop_t, skip_sample_adjustment=skip_sample_adjustment,
-                     draft_row_stats=dstats[:g] if stash else None,
-                     draft_row_keep=dkeep[:g] if dkeep is not None else None)
+                     draft_row_stats=dstats[:g] if stash else None)
         n, x, status, stop_index = (int(v) for v in torch.stack([
             out.n_accepted[0].long(), out.next_token[0], out.row_status[0].long(), out.stop_index[0].long()]).tolist())
         if status & _lib.SD_ROW_INVALID_DIST:

@@ -311,3 +311,71 @@ def test_verify_with_draw_keeps(sd, proc, dtype, V):
         DRAW_CLOSE_CALLS.append(f"keep {proc.kind} row={s} draft={i} p/q={ratio:.9g} u={u:.9g}")
     with pytest.raises(ValueError):   # keeps come with the stats
         sd.ops.verify(trows, drows, ids, r, spec, spec, sd.PhiloxNoise(seed=13), draft_row_keep=keeps)
+
+
+def nucleus_case(kind, V, dtype, seed):
+    g = torch.Generator().manual_seed(seed)
+    if kind == "peaked":        # ~30 hot tokens carry the mass
+        x = peaked_logits(V, 30, seed, dtype).float()
+    elif kind == "ties":        # few distinct values: the cut falls inside a run of equal values
+        x = (torch.randint(0, 6, (V,), generator=g).float() * 0.75)
+        x[torch.randperm(V, generator=g)[:40]] += 9.0
+    else:                       # the bench's Llama-3 shaped rows (std 3): the nucleus holds thousands
+        x = torch.randn(V, generator=g) * 3.0
+    return x.to(dtype)
+
+
+@pytest.mark.parametrize("kind,V,dtype,T,top_p", [
+    ("peaked", 128256, torch.bfloat16, 1.0, 0.9), ("peaked", 32000, torch.float16, 0.7, 0.9),
+    ("ties", 128256, torch.bfloat16, 1.0, 0.8), ("peaked", 50257, torch.bfloat16, 1.0, 0.5),
+    ("peaked", 4096, torch.bfloat16, 0.9, 0.95)])
+def test_nucleus_rejection_draw(sd, kind, V, dtype, T, top_p):
+    """k_draw_nuc (sample_rows of a nucleus processor without token_prob / row_stats / row_keep,
+    PHILOX, top_p >= 0.5, T <= 1): draws from the whole row's softmax and keeps a draw iff the
+    T = 1 mass before it does not cross top_p.  The draws follow the processed distribution
+    (utils/logits_processor.py:66-81 + :39-49; chi-square, never a token outside the nucleus)."""
+    x = nucleus_case(kind, V, dtype, 3 + V % 97)
+    proc = ref.Processor("nucleus", T, 0, top_p)
+    spec = spec_of(sd, proc)
+    R, calls = 8, 128      # 8 rows x 16 slices: the whole grid resident (one 1024-thread slice per CU)
+    rows = x.view(1, -1).repeat(R, 1).to(DEV)
+    noise = sd.PhiloxNoise(seed=1234)
+    samples = []
+    for _ in range(calls):
+        tok, prob, st = sd.ops.sample_rows(rows, spec, noise)
+        assert prob is None
+        stc = st.cpu()
+        assert bool(((stc & sd.lib.SD_ROW_DONE) != 0).all()) and not bool((stc & 0x40).any())
+        samples += tok.cpu().tolist()
+    # the nucleus the verify's threshold search cuts for this row (k_thr_hist, the same slice
+    # normaliser; test_gpu_threshold holds it to the exact oracle): every draw inside it, and the
+    # draws distributed as the processed softmax over it
+    keep = torch.empty(R, 4, dtype=torch.int32, device=DEV)
+    sd.ops.sample_rows(rows, spec, sd.PhiloxNoise(seed=5), row_stats_out=torch.empty(R, 2, device=DEV),
+                       row_keep_out=keep)
+    kc = keep.cpu()
+    assert all(torch.equal(kc[i], kc[0]) for i in range(R))
+    tau, tie = float(kc[0, 0:1].view(torch.float32)), int(kc[0, 1])
+    xf = x.float()
+    j = torch.arange(V)
+    kept = (xf > tau) | ((xf == tau) & (j <= tie))
+    y = (xf / T).to(dtype).double() if T != 1.0 else xf.double()
+    want = torch.where(kept, torch.exp(y - y[kept].max()), torch.zeros_like(y))
+    chi2_check(samples, (want / want.sum()).numpy(), f"nucleus-reject {kind} V={V}")
+    # and the cut is the exact oracle's (the rows here sit far from rounding boundaries)
+    orow = x.float() if dtype == torch.float16 else x
+    exact = ref.processed_logits(orow.view(1, -1), dataclasses.replace(proc, stable_ties=True), exact=True)[0]
+    assert int(kept.sum()) == int((exact.float() > -1e19).sum())
+
+
+def test_nucleus_rejection_draw_flags_bad_rows(sd):
+    x = torch.randn(3, 128256).to(torch.bfloat16)
+    x[1, 5] = float("nan")
+    x[2, 77] = float("inf")
+    x[0, 9] = float("-inf")   # -inf is a zero-probability token, not an error
+    spec = sd.ops.ProcSpec("nucleus", 1.0, 0, 0.9)
+    tok, _, st = sd.ops.sample_rows(x.to(DEV), spec, sd.PhiloxNoise(seed=3))
+    st, tok = st.cpu(), tok.cpu()
+    assert int(st[0]) & 0x40 == 0 and int(tok[0]) != 9
+    assert int(st[1]) & 0x40 and int(st[2]) & 0x40
+    assert int(tok[1]) == -1 and int(tok[2]) == -1
