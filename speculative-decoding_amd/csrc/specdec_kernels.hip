@@ -2792,8 +2792,9 @@ int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* strea
     if (P.token_prob || P.row_stats || P.keep_out) return 0;
     if (const char* e = getenv("SD_NUC_REJECT"))
         if (!atoi(e)) return 0;
-    const int nsl = (P.V + sd::kThrSlice - 1) / sd::kThrSlice;
-    if (nsl > kWave || P.B > kCntMax) return 0;
+    // the verify's threshold search must cut this row with the same normaliser: its sub-slice mode
+    const int nsl = (P.V + sd::kNucSlice - 1) / sd::kNucSlice;
+    if (nsl > kWave || P.B > kCntMax || sd::kThrSlice != 4 * sd::kSubSlice) return 0;
     // the records (kNucRecs x 16 B per slice) inside the row's share of the ResPart region
     if ((int64_t)nsl * sd::kNucRecs * 16 > (int64_t)(max_chunks(P.V) + 1) * (int64_t)sizeof(sd::ResPart)) return 0;
     static int cap[64];
@@ -2801,7 +2802,7 @@ int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* strea
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
     if (cap[dev] == 0) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sd::k_draw_nuc<SD_BF16>, sd::kThrThreads, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sd::k_draw_nuc<SD_BF16>, sd::kNucThreads, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             per_cu = cus = 0;
         cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
@@ -2823,9 +2824,9 @@ int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* strea
     A.top_p = proc.top_p;
     const dim3 grid(nsl, P.B);
     if (P.tdt == SD_BF16)
-        hipLaunchKernelGGL(sd::k_draw_nuc<SD_BF16>, grid, dim3(sd::kThrThreads), 0, (hipStream_t)stream, A);
+        hipLaunchKernelGGL(sd::k_draw_nuc<SD_BF16>, grid, dim3(sd::kNucThreads), 0, (hipStream_t)stream, A);
     else
-        hipLaunchKernelGGL(sd::k_draw_nuc<SD_F16>, grid, dim3(sd::kThrThreads), 0, (hipStream_t)stream, A);
+        hipLaunchKernelGGL(sd::k_draw_nuc<SD_F16>, grid, dim3(sd::kNucThreads), 0, (hipStream_t)stream, A);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) { g_last_error = e; return SD_ERR_LAUNCH; }
     return 1;
