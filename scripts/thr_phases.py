@@ -1,7 +1,9 @@
-"""Per-workgroup phase timing of the 16-bit threshold kernel (k_thr_hist, poll mode) for the
-configs[1] drafter draw: one nucleus-0.9 row of 128256 bf16 (diagnostic; GPU box, the
-SD_PHASE_TIMING build: make -C speculative-decoding_amd timing).  Prints when the row's slice
-workgroups reach each phase, µs after the first start (s_memrealtime, 100 MHz)."""
+"""Per-workgroup phase timing of a configs[1] nucleus-0.9 drafter draw, one row of 128256 bf16
+(diagnostic; GPU box, the SD_PHASE_TIMING build: make -C speculative-decoding_amd timing):
+the threshold search (k_thr_hist, poll mode; the draw asks for row stats, so the threshold + k_draw
+path runs) or, with THR_NUC=1, the rejection draw (k_draw_nuc).  THR_ROWS sets the row count.
+Prints when the row's slice workgroups reach each phase, µs after the first start
+(s_memrealtime, 100 MHz)."""
 import os
 import sys
 
