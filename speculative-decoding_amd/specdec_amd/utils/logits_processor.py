@@ -61,6 +61,11 @@ class MultinomialProcessor(LogitsProcessor):
         super().__init__(temperature)
 
     def sample(self, probs: Tensor) -> Tensor:
+        """The reference's own call (utils/logits_processor.py:48-49), for callers that sample
+        ``proc(logits)`` outside the loops.  On a GPU tensor it draws from torch's device
+        generator, so it is NOT the bit-exact draw of the CPU reference; the drop-in loops never
+        call it — their draws go through ``sd_sample`` / ``sd_verify`` (STREAM mode for
+        torch-generator bit-exactness, ``specdec_amd.noise``)."""
         return torch.multinomial(probs, num_samples=1)
 
 
