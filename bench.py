@@ -11,16 +11,19 @@ and the per-row outputs).  Every logit row is read once by the step, plus the tw
 residual samples from.  Independent prompt batches shard data-parallel (one replica per GPU,
 no collective on the data path), so scaling is weak: every rank verifies its own 32 rows.
 
-value = output tokens (accepted drafts + resampled tokens, all ranks) / max-over-ranks wall
-time of the K timed steps.  Steps run as hipGraph replays (the step is captured once per
-`--graph-steps` steps), noise is in-kernel Philox (perf mode).  Also reported in the same line:
-acceptance rate (engine/metrics.py:123-129), per-kernel timings with the HBM roofline of the
-step's DOMINANT kernel (the largest per-step share; HIP events on the launch stream,
-algorithmic bytes = every logit row the kernel must read, once), the same step in STREAM mode
-(the reference's torch-generator noise, bit-exact tokens), the strong-scaling variant of
-configs[2] (a global batch of --batch rows split over the ranks) when N > 1, the configs[1]
-batch-1 step latencies, and the CPU baseline = the oracle (reference semantics, torch-CPU)
-timed on a bounded sample of the same workload on this host.
+value = output tokens (accepted drafts + resampled tokens, all ranks, counted exactly by the
+verify kernel itself: sd_verify_args.row_counts) / max-over-ranks wall time of the K timed steps.
+Steps run as hipGraph replays — the K steps are >= 5 back-to-back replays of one captured graph,
+each also timed by HIP events (median reported) — and noise is in-kernel Philox (perf mode).
+Also reported in the same line: acceptance rate (engine/metrics.py:123-129) over >= 200 untimed
+steps, per-kernel timings with the HBM roofline of the step's DOMINANT kernel (the largest
+per-step share; HIP events on the launch stream, algorithmic bytes = every logit row the kernel
+must read, once), the same step in STREAM mode (the reference's torch-generator noise, bit-exact
+tokens, in a noise session as the drop-in engine runs it), the strong-scaling variant of
+configs[2] (a global batch of --batch rows split over the ranks) when N > 1 and its 16 / 8 / 4-row
+shards measured on one GPU when N = 1, the configs[1] batch-1 step latencies, the configs[4]
+n-gram verify step, and the CPU baseline = the oracle (reference semantics, torch-CPU) timed on a
+bounded sample of the same workload on this host.
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
@@ -59,7 +62,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stream-steps", type=int, default=5, help="STREAM-mode (bit-exact noise) steps; 0 = skip")
-    ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] batch-1 lines")
+    ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] / configs[4] batch-1 lines")
+    ap.add_argument("--no-shards", action="store_true", help="skip the 16 / 8 / 4-row shard lines")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsing N ranks on fewer GPUs)")
     return ap.parse_args()
@@ -69,12 +73,13 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def graph_steps(step, steps, per_graph, noise=None, calls_per_step=0):
-    """Capture `per_graph` steps in one hipGraph, replay steps // per_graph times (untimed warm replay
-    first).  Returns (graph, outputs of the captured steps, replays).  With a PhiloxNoise that has
-    a device counter base, the graph ends by moving it past the captured calls, so every replay
-    draws fresh noise (the outputs are those of the last replay)."""
-    G = max(1, min(per_graph, steps))
+def graph_steps(step, steps, per_graph, noise=None, calls_per_step=0, min_replays=1):
+    """Capture G steps in one hipGraph (G <= per_graph, G divides steps, and at least min_replays
+    replays when steps allows), replay once untimed.  Returns (graph, outputs of the captured
+    steps, replays).  With a PhiloxNoise that has a device counter base, the graph ends by moving
+    it past the captured calls, so every replay draws fresh noise (the outputs are those of the
+    last replay)."""
+    G = max(1, min(per_graph, steps, steps // max(min_replays, 1) or 1))
     while steps % G:
         G -= 1
     graph = torch.cuda.CUDAGraph()
@@ -89,17 +94,28 @@ def graph_steps(step, steps, per_graph, noise=None, calls_per_step=0):
     return graph, outs, steps // G
 
 
-def timed_replays(graph, replays, dist):
+def timed_replays(graph, replays, dist, per_replay=None):
+    """Wall time of `replays` back-to-back replays, bracketed by a barrier and a device sync on both
+    sides.  per_replay (a list): receives each replay's device time in ms, from HIP events recorded
+    on the launch stream between the replays (no sync inside the timed region)."""
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(replays + 1)] if per_replay is not None else None
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(replays):
+    if evs:
+        evs[0].record()
+    for i in range(replays):
         graph.replay()
+        if evs:
+            evs[i + 1].record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
-    return time.perf_counter() - t0
+    elapsed = time.perf_counter() - t0
+    if evs:
+        per_replay.extend(evs[i].elapsed_time(evs[i + 1]) for i in range(replays))
+    return elapsed
 
 
 def engine_logits(B, g, V, sigma, seed, dev):
@@ -125,6 +141,9 @@ class EngineStep:
         self.stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
         self.trows = [tl[:, t, :] for t in range(g)]
         self.drows = [dl[:, t, :] for t in range(g)]
+        # per row (accepted drafts, tokens emitted), accumulated by the verify kernel itself: every
+        # timed step's tokens are counted exactly, with no extra launch (sd_verify_args.row_counts)
+        self.counts = torch.zeros(B, 2, dtype=torch.long, device=dev)
 
     def draw(self, d):
         self.ops.sample_rows(self.drows[d], self.ops.PLAIN_SOFTMAX, self.noise, tokens_out=self.draft[:, d],
@@ -138,19 +157,24 @@ class EngineStep:
         ops = self.ops
         return ops.verify(self.trows, self.drows, self.draft, self.lib.SD_RULE_ENGINE, ops.PLAIN_SOFTMAX,
                           ops.PLAIN_SOFTMAX, self.noise, self.stops, prof_events=prof, row_base=self.row0,
-                          draft_row_stats=self.dstats if self.stash else None)
+                          draft_row_stats=self.dstats if self.stash else None, row_counts=self.counts)
+
+    def reserve(self):
+        """STREAM: the step's words in one generation (γ draws of 2·B·V, the verify's <= B·(γ+2V)),
+        as the drop-in engine reserves a window's words (noise.StreamNoise.reserve)."""
+        if hasattr(self.noise, "reserve"):
+            self.noise.reserve(self.g * 2 * self.B * self.V + self.B * (self.g + 2 * self.V), self.trows[0].device)
 
     def __call__(self, prof=None):
+        self.reserve()
         self.draws()
         return self.verify(prof)
 
-
-def row_counts(outs, _lib):
-    """(tokens, per-row accepted counts) of a list of VerifyOut (engine rule: no bonus token;
-    a reject adds the resampled token)."""
-    acc = torch.stack([o.n_accepted.long() for o in outs]).sum(0).cpu()
-    resid = sum(int(((o.row_status & _lib.SD_ROW_RESIDUAL) != 0).sum()) for o in outs)
-    return int(acc.sum()) + resid, acc
+    def read_counts(self):
+        """(accepted drafts, tokens emitted) per row since the last reset, and reset."""
+        c = self.counts.cpu()
+        self.counts.zero_()
+        return c
 
 
 def positive_rate_sums(acc_rows, drafted_per_row):
@@ -213,19 +237,32 @@ def main():
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
-    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps, noise, g + 1)
+    # the K timed steps: >= 5 replays of one captured graph (G steps each), event-timed one by one
+    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps, noise, g + 1, min_replays=5)
     G = len(outs)
-    elapsed = timed_replays(graph, replays, dist)
+    step.read_counts()                                   # drop the warm-up / capture replay's counts
+    replay_ms = []
+    elapsed = timed_replays(graph, replays, dist, replay_ms)
+    counts = step.read_counts()                          # exact: every timed step's tokens
+    tokens_t, acc_t = int(counts[:, 1].sum()), counts[:, 0]
+    rsum_t, rcnt_t = positive_rate_sums(acc_t, g * args.steps)
+
+    # acceptance over a larger untimed sample (>= 200 steps of the same graph, fresh noise each)
+    n_count = max(1, -(-max(200, args.steps) // G))
+    for _ in range(n_count):
+        graph.replay()
+    counts_c = step.read_counts()
+    rsum, rcnt = positive_rate_sums(counts_c[:, 0], g * G * n_count)
 
     # the verify alone (on the captured draws' outputs), for the per-phase breakdown
-    vgraph, _, _ = graph_steps(step.verify, args.steps, args.graph_steps)
-    verify_ms = timed_replays(vgraph, replays, None) / args.steps * 1e3
+    vgraph, _, vrep = graph_steps(step.verify, args.steps, args.graph_steps)
+    verify_ms = timed_replays(vgraph, vrep, None) / args.steps * 1e3
 
-    tokens_g, acc_rows = row_counts(outs, _lib)
-    rsum, rcnt = positive_rate_sums(acc_rows, g * G)
-    elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens_g * replays, "accepted": float(acc_rows.sum()) * replays,
-                                          "drafted": B * g * G * replays, "rate_sum": rsum, "rate_cnt": rcnt},
-                                dev, dist)
+    elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens_t, "accepted": float(acc_t.sum()),
+                                          "drafted": B * g * args.steps, "rate_sum": rsum, "rate_cnt": rcnt,
+                                          "rate_sum_t": rsum_t, "rate_cnt_t": rcnt_t,
+                                          "accepted_c": float(counts_c[:, 0].sum()),
+                                          "drafted_c": B * g * G * n_count}, dev, dist)
 
     # per-kernel timing (HIP events on the launch stream, back-to-back launches so the event pair's
     # own cost is amortised): k_draw (one per drafter draw), k_stats (sd_verify's prof hook, with its
@@ -265,19 +302,26 @@ def main():
         for _ in range(max(args.warmup, 1)):
             sstep()
         torch.cuda.synchronize()
-        sgraph, souts, sreplays = graph_steps(sstep, args.steps, args.graph_steps, snoise, g + 1)
+        sgraph, souts, sreplays = graph_steps(sstep, args.steps, args.graph_steps, snoise, g + 1, min_replays=5)
+        sstep.read_counts()
         selapsed = timed_replays(sgraph, sreplays, dist)
-        stoks, _ = row_counts(souts, _lib)
-        selapsed, stot = dp.aggregate(selapsed, {"tokens": stoks * sreplays}, dev, dist)
+        stoks = int(sstep.read_counts()[:, 1].sum())
+        selapsed, stot = dp.aggregate(selapsed, {"tokens": stoks}, dev, dist)
         strong = {"value": stot["tokens"] / selapsed, "unit": "tokens/s", "global_batch": args.batch,
                   "rows_per_gpu": s1 - s0, "ms_per_step": selapsed / args.steps * 1e3}
+
+    # configs[2]'s strong-scaling shards measured on this GPU: 32 / N rows per GPU at N = 2, 4, 8
+    shards = None
+    if rank == 0 and world == 1 and not args.no_shards:
+        shards = shard_lines(tl, dl, args, ops, _lib, PhiloxNoise, EngineStep)
 
     stream = None
     if rank == 0 and args.stream_steps > 0:
         stream = stream_line(tl, dl, row0, args, ops, _lib, StreamNoise)
-    cfg1 = None
+    cfg1 = cfg4 = None
     if rank == 0 and world == 1 and not args.no_configs1:
         cfg1 = configs1_lines(dev, args, ops, _lib, PhiloxNoise)
+        cfg4 = configs4_line(dev, args, ops, _lib, PhiloxNoise)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(tl, dl, step.draft, args)
@@ -310,10 +354,19 @@ def main():
             "config": {"workload": "configs[2]: Llama-3-8B/3.2-1B logit shapes, engine step sampling path: "
                                    "γ drafter draws + verify (rule A10)",
                        "rows_per_gpu": args.batch, "global_batch": args.batch * world, "gamma": g, "vocab": V,
-                       "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G},
-            # engine/metrics.py:123-129: mean of per-row acc/tot over the rows with a positive rate
+                       "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G, "replays": replays},
+            # engine/metrics.py:123-129: mean of per-row acc/tot over the rows with a positive rate,
+            # over >= 200 untimed steps of the same graph (the timed steps' own figure beside it)
             "acceptance_rate": tot["rate_sum"] / tot["rate_cnt"] if tot["rate_cnt"] else 0.0,
-            "acceptance_rate_pooled": tot["accepted"] / tot["drafted"],
+            "acceptance_rate_pooled": tot["accepted_c"] / tot["drafted_c"],
+            "acceptance_steps": G * n_count,
+            "acceptance_rate_timed": tot["rate_sum_t"] / tot["rate_cnt_t"] if tot["rate_cnt_t"] else 0.0,
+            "tokens_timed": tot["tokens"],
+            "replays": {"count": replays, "steps_per_replay": G,
+                        "ms_median": statistics.median(replay_ms), "ms_min": min(replay_ms),
+                        "ms_max": max(replay_ms),
+                        "ms_per_step_median": statistics.median(replay_ms) / G,
+                        "note": "HIP events between back-to-back replays of the captured steps (rank 0)"},
             "roofline": {"bound": "hbm", "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": dk["frac"], "traffic": traffic,
                          "kernel": dominant, "kernel_ms": dk["ms"], "launches_per_step": dk["launches_per_step"],
@@ -325,7 +378,9 @@ def main():
             "phases_ms": {"draws": ms_per_step - verify_ms, "verify": verify_ms},
             "stream": stream,
             "strong_scaling": strong,
+            "shard_rows": shards,
             "configs1": cfg1,
+            "configs4": cfg4,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -335,25 +390,88 @@ def main():
 
 def stream_line(tl, dl, row0, args, ops, _lib, StreamNoise):
     """The same engine step in STREAM mode: the noise is the reference's own torch CPU generator
-    stream (bit-exact tokens under torch.manual_seed), eager steps (the generator is advanced
-    by the words each verify consumed)."""
+    stream (bit-exact tokens under torch.manual_seed), run as the drop-in engine runs it — inside
+    a noise session (the generator state stays on the device) with one word reservation per step
+    (StreamNoise.reserve: one jump-ahead + generation for the γ draws and the verify).  Eager
+    steps: the session's host bookkeeping sits between the calls."""
     gen = torch.Generator().manual_seed(1234)
-    step = EngineStep(tl, dl, StreamNoise(gen), row0, ops, _lib)
-    B, g = step.B, step.g
-    step()
-    torch.cuda.synchronize()
-    outs = []
-    t0 = time.perf_counter()
-    for _ in range(args.stream_steps):
-        outs.append(step())
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    tokens, acc_rows = row_counts(outs, _lib)
-    rsum, rcnt = positive_rate_sums(acc_rows, g * len(outs))
+    noise = StreamNoise(gen)
+    step = EngineStep(tl, dl, noise, row0, ops, _lib)
+    B, g, V = step.B, step.g, step.V
+    with noise.session():
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        step.read_counts()
+        t0 = time.perf_counter()
+        for _ in range(args.stream_steps):
+            step()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        c = step.read_counts()
+    tokens = int(c[:, 1].sum())
+    rsum, rcnt = positive_rate_sums(c[:, 0], g * args.stream_steps)
     ms = dt / args.stream_steps * 1e3
+    words = g * 2 * B * V + B * (g + 2 * V)          # reserved per step (the verify's worst case)
     return {"noise": "stream", "value": tokens / dt, "unit": "tokens/s", "ms_per_step": ms,
             "steps": args.stream_steps, "rows": B, "acceptance_rate": rsum / rcnt if rcnt else 0.0,
-            "note": "torch CPU generator words (bit-exact with the reference), eager steps"}
+            "logit_bytes_per_step": 2 * g * B * V * 2, "noise_words_per_step": words,
+            "noise_bytes_per_step": words * 4 * 2,
+            "note": "torch CPU generator words (bit-exact with the reference) made on the GPU, one reservation "
+                    "per step in a noise session (as the drop-in engine); noise bytes = words written + read"}
+
+
+def shard_lines(tl, dl, args, ops, _lib, PhiloxNoise, EngineStep):
+    """configs[2] as written is a GLOBAL batch of 32 rows over N GPUs: 16 / 8 / 4 rows per GPU at
+    N = 2 / 4 / 8.  One GPU times the engine step at each shard size (hipGraph replays), which
+    bounds the strong-scaling curve: projected N-GPU tokens/s = N x the shard's tokens/s."""
+    res = {}
+    for rows in (16, 8, 4):
+        if rows >= tl.shape[0]:
+            continue
+        noise = PhiloxNoise(seed=4545 + rows, offset_dev=torch.zeros(1, dtype=torch.long, device=tl.device))
+        st = EngineStep(tl[:rows], dl[:rows], noise, 0, ops, _lib)
+        for _ in range(3):
+            st()
+        torch.cuda.synchronize()
+        steps = 100
+        graph, _, replays = graph_steps(st, steps, 20, noise, st.g + 1, min_replays=5)
+        st.read_counts()
+        dt = timed_replays(graph, replays, None)
+        tokens = int(st.read_counts()[:, 1].sum())
+        n_gpus = args.batch // rows
+        res[f"rows{rows}"] = {"rows_per_gpu": rows, "n_gpus_for_global_32": n_gpus,
+                              "ms_per_step": dt / steps * 1e3, "tokens_per_s_per_gpu": tokens / dt,
+                              "projected_global_tokens_per_s": n_gpus * tokens / dt}
+    return res
+
+
+def configs4_line(dev, args, ops, _lib, PhiloxNoise):
+    """configs[4]: the n-gram-assisted verify step (ngram_assisted/ngram_assisted.py:104-141, rule
+    A11) — γ=8, top-p 0.9, filler top-3 over 9 synthetic Llama-3 shaped target rows (batch 1),
+    drafts the target agrees with; hipGraph replays, Philox noise."""
+    g, V = 8, args.vocab
+    gen = torch.Generator(device=dev).manual_seed(21)
+    tl = (torch.randn(1, g + 1, V, generator=gen, device=dev) * 3.0).to(torch.bfloat16)
+    draft = tl[0, :g].float().argmax(-1).unsqueeze(0).contiguous()
+    stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
+    proc = ops.ProcSpec("nucleus", 1.0, 0, 0.9)
+    noise = PhiloxNoise(seed=9, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
+    trows = [tl[:, t] for t in range(g + 1)]
+
+    def step():
+        return ops.ngram_verify(trows, draft, proc, noise, stops, filler_k=3)
+
+    for _ in range(5):
+        step()
+    torch.cuda.synchronize()
+    graph, outs, replays = graph_steps(step, 200, 20, noise, 1)
+    dt = timed_replays(graph, replays, None)
+    n = torch.stack([o.n_accepted.long() for o in outs]).sum().item()
+    steps = len(outs) * replays
+    return {"us_per_step": dt / steps * 1e6, "tokens_per_s": (n + len(outs)) * replays / dt,
+            "accepted_per_step": n / len(outs), "alg_bytes_per_step": (g + 1) * V * 2,
+            "gamma": g, "top_p": 0.9, "filler_top_k": 3, "rule": "A11"}
 
 
 def configs1_lines(dev, args, ops, _lib, PhiloxNoise):

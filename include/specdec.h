@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 7
+#define SD_ABI_VERSION 8
 #define SD_MAX_GAMMA 16
 
 typedef enum {
@@ -108,6 +108,12 @@ typedef struct {
 #define SD_ROW_EXCHANGE_TIMEOUT 0x200 /* a workgroup's partial never arrived within the bounded
                                        wait of an in-launch exchange (k_draw_lean); the row's
                                        outputs are invalid (also flagged SD_ROW_INVALID_DIST)    */
+/* The bits that make a row's outputs unusable: the reference raises in these cases (torch.multinomial
+ * on NaN / inf / zero mass, engine/infer_engine.py:246,321-325; sampling/speculative_decoding.py:171),
+ * so callers must treat them as errors, never as tokens.  Every entry point that takes a
+ * `status_or` word ORs the error bits of each of its rows into it (one device atomic per failed
+ * row; nothing on the success path), so a decode loop can test ONE word where it already syncs. */
+#define SD_ROW_ERROR_MASK (SD_ROW_INVALID_DIST | SD_ROW_NOISE_OVERRUN | SD_ROW_EXCHANGE_TIMEOUT)
 
 /* A top-k / nucleus row's keep predicate (the threshold search's result): token j is kept iff
  * x_j > tau || (x_j == tau && j <= tie_idx), x_j the row's logit (tau = -inf, tie_idx = INT_MAX
@@ -200,6 +206,14 @@ typedef struct {
        thresholds: the keep is a function of the row and draft_proc alone, so the draw's equals
        the one the verify would compute (utils/logits_processor.py:52-101).                    */
     const struct sd_row_keep* draft_row_keep;
+    /* optional (nullable): device int32 [1]; the call ORs every row's SD_ROW_ERROR_MASK bits into
+       it (never cleared by the library: the caller zeroes it, e.g. once per decode loop)        */
+    int32_t* status_or;
+    /* optional (nullable): device int64 [B, 2]; the call ADDS (accepted drafts n, tokens emitted)
+       to row b's pair — emitted = n plus the resampled / bonus token when one was drawn.  The
+       acceptance / throughput bookkeeping (engine/infer_engine.py:258,308; engine/metrics.py:100-129)
+       kept on the device with no extra launch.                                                  */
+    int64_t* row_counts;
 } sd_verify_args;
 
 typedef struct {
@@ -224,6 +238,7 @@ typedef struct {
     struct sd_row_keep* row_keep; /* [R] keep predicate of each row under a top-k / nucleus
                                     processor, the input sd_verify takes as draft_row_keep
                                     (nullable; not written for other processors)               */
+    int32_t* status_or;          /* [1] (nullable): every row's SD_ROW_ERROR_MASK bits ORed in    */
 } sd_sample_args;
 
 /* LogitsProcessor.__call__ (utils/logits_processor.py:13-15) materialised: probs = softmax(_process(l)/T)
@@ -243,6 +258,18 @@ typedef struct {
 
 int32_t sd_abi_version(void);
 const char* sd_status_string(int32_t status);
+
+/* In-launch exchanges.  Several kernels exchange per-row partials inside ONE launch by polling
+ * tagged records ("poll mode"; k_draw_lean, k_draw_nuc, k_thr_hist, the k_stats / k_sample tails)
+ * when the host's occupancy check says the whole grid is resident.  A grid that shares the GPU
+ * with other work (another process, RCCL kernels, a side stream) may not be: the bounded polls
+ * then flag rows SD_ROW_EXCHANGE_TIMEOUT.  allow_poll = 0 selects the arrival-counter exchanges
+ * everywhere (no kernel waits on another workgroup); 1 (default) lets the occupancy check decide.
+ * spin_limit bounds every poll (re-reads with s_sleep between them; 0 = the default 65536, < 0 =
+ * give up at once — a test hook that forces the timeout path).  Process-wide; the environment
+ * variables SD_POLL (0/1) and SD_POLL_SPIN_LIMIT set the initial values.                       */
+int32_t sd_set_poll_policy(int32_t allow_poll, int32_t spin_limit);
+int32_t sd_get_poll_policy(int32_t* allow_poll, int32_t* spin_limit);
 const char* sd_last_hip_error(void);   /* hipGetErrorString of the last failed launch (this thread) */
 
 /* Workspaces: device memory of at least sd_*_workspace_size bytes, ZERO-FILLED ONCE when
@@ -294,6 +321,7 @@ typedef struct {
     int64_t filler_stride_b;
     void* workspace;
     size_t workspace_bytes;
+    int32_t* status_or;          /* [1] (nullable): every row's SD_ROW_ERROR_MASK bits ORed in    */
 } sd_ngram_args;
 
 size_t sd_ngram_workspace_size(int32_t batch, int32_t gamma, int32_t vocab);
@@ -389,7 +417,9 @@ int32_t sd_mt19937_jump_table(int64_t stride_words, int32_t count, uint64_t* out
 int32_t sd_mt19937_char_poly(uint64_t* out, size_t words);                         /* >= 313 words           */
 int32_t sd_mt19937_fill_substreams(const uint32_t* block, int32_t tau0, uint32_t* out, int64_t n,
                                    int64_t stride_words, const uint64_t* table, int32_t count);
-/* device */
+/* device.  sd_mt19937_commit moves the state past `used` + *used_dev words (used_dev nullable): a
+ * host-known prefix (e.g. the draws of an engine window, 2·B·V words each) plus the count a verify
+ * wrote on the device.                                                                           */
 size_t sd_mt19937_generate_workspace_size(int64_t n_words, int64_t stride_words);
 int32_t sd_mt19937_generate(const sd_mt_generate_args* args, void* stream);
 int32_t sd_mt19937_commit(sd_mt_state* state, const uint32_t* words, int64_t n_words, const int64_t* used_dev,

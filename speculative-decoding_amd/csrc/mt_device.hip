@@ -176,7 +176,7 @@ __global__ void __launch_bounds__(256) k_mt_commit(sd_mt_state* __restrict__ st,
                                                    int64_t n_words, const int64_t* __restrict__ used_dev, int64_t used,
                                                    int32_t* __restrict__ status) {
     const int t = threadIdx.x;
-    const int64_t u = used_dev ? used_dev[0] : used;
+    const int64_t u = used + (used_dev ? used_dev[0] : 0);   // host-known prefix + the device count
     const int tau0 = st->tau0;
     __syncthreads();                                       // every thread has read tau0
     if (u <= 0) return;
@@ -235,7 +235,7 @@ int32_t sd_mt19937_generate(const sd_mt_generate_args* a, void* stream) {
 
 int32_t sd_mt19937_commit(sd_mt_state* state, const uint32_t* words, int64_t n_words, const int64_t* used_dev,
                           int64_t used, int32_t* status, void* stream) {
-    if (!state || n_words < 0 || (n_words > 0 && !words) || (!used_dev && used < 0)) return SD_ERR_INVALID;
+    if (!state || n_words < 0 || (n_words > 0 && !words) || used < 0) return SD_ERR_INVALID;
     hipLaunchKernelGGL(k_mt_commit, dim3(1), dim3(256), 0, (hipStream_t)stream, state, words, n_words, used_dev, used,
                        status);
     return launch_ok() ? SD_OK : SD_ERR_LAUNCH;

@@ -229,6 +229,18 @@ __device__ __forceinline__ void coh_wait() {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
 }
 
+// A row's error bits (SD_ROW_ERROR_MASK) into the caller's sticky word: one device atomic, and
+// only for a failed row (the success path issues nothing).  Called by the one thread that writes
+// the row's status.
+__device__ __forceinline__ void flag_error(int32_t* acc, int32_t status) {
+    const int32_t e = status & SD_ROW_ERROR_MASK;
+    if (acc && e) __hip_atomic_fetch_or(acc, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bounded polls: `limit` re-reads at most (the host's spin limit, sd_set_poll_policy); a negative
+// limit gives up at once (tests force the timeout path with it).
+__device__ __forceinline__ bool spin_more(int spin, int limit) { return spin < limit; }
+
 // ---------------------------------------------------------------- exp
 // e^x with v_exp_f32 (2^t) and the rounding error of t = x*log2(e) folded back in by FMA:
 // ~1 ulp like ocml's expf but without its range/denormal branches.  Every kernel uses this

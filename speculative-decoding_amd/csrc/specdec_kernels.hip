@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <map>
+#include <atomic>
 #include <mutex>
 #include <type_traits>
 
@@ -118,6 +119,9 @@ struct Plan {
     int32_t spoll;        // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
     int32_t kpoll;        // k_stats (decide tail): poll-mode partials (tagged records, no counter)
     int32_t thr_poll;     // k_thr_hist: slice maxima exchanged in-launch (no k_thr_max launch)
+    int32_t spin_limit;   // poll modes: re-reads before a record counts as lost (sd_set_poll_policy)
+    int32_t* status_or;   // caller's sticky error word (nullable): every row's SD_ROW_ERROR_MASK bits
+    int64_t* row_counts;  // sd_verify (nullable): per row += (accepted n, tokens emitted)
     // sd_ngram_verify (sd_ngram.inc)
     struct NgPart* ngpart;
     int64_t* filler_ids;
@@ -337,6 +341,18 @@ __device__ __forceinline__ bool arrive_last(uint32_t* ctr, uint32_t total) {
     coh_wait();
     const uint32_t prev = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (prev + 1u != total) return false;
+    __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+}
+
+// arrive_last for <= 65535 arrivals that each carry a flag (high half of the counter): *any says
+// whether some arrival set its flag (written for the last arrival only)
+__device__ __forceinline__ bool arrive_last_f(uint32_t* ctr, uint32_t total, bool flag, bool* any) {
+    coh_wait();
+    const uint32_t add = 1u + (flag ? 0x10000u : 0u);
+    const uint32_t now = __hip_atomic_fetch_add(ctr, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + add;
+    if ((now & 0xffffu) != total) return false;
+    *any = (now >> 16) != 0u;
     __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return true;
 }
@@ -854,7 +870,7 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, D
                     const uint4* rp = stats_rec(P, b, s, lane);
                     const uint32_t tag = stats_tag(ep, b, s, lane);
                     uint4 r = ld_coh16(rp);
-                    for (int spin = 0; r.z != tag && spin < (1 << 16); ++spin) {
+                    for (int spin = 0; r.z != tag && spin_more(spin, P.spin_limit); ++spin) {
                         __builtin_amdgcn_s_sleep(1);
                         r = ld_coh16(rp);
                     }
@@ -1166,8 +1182,9 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
             wave_argmax(bv, bi);
             x = bi;
             status = (status & ~SD_ROW_RESIDUAL) | SD_ROW_FALLBACK_P;
-        } else if (s == 0.f) {
-            // max_fn divides by zero: all-NaN distribution
+        } else if (s == 0.f || (P.t_stoch && !(s > 0.f && s < INFINITY))) {
+            // max_fn divides by zero (all-NaN distribution) or by NaN / inf: torch raises
+            // (sampling/speculative_decoding.py:171; engine/infer_engine.py:325 with den NaN)
             if (P.t_stoch) status |= SD_ROW_INVALID_DIST;
             else x = 0;   // torch.argmax over an all-NaN row
         } else {
@@ -1228,6 +1245,10 @@ __device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, f
         }
         wave_argmax(pv, pi);
         x = pi;
+        // multinomial over a row whose softmax is NaN / inf (a NaN or +inf logit): torch raises
+        // (utils/logits_processor.py:48-49); torch.argmax (greedy) does not
+        const float2 ms = P.rowstat[b * P.slots + d.slot];
+        if (P.t_stoch && !(ms.y > 0.f && ms.y < INFINITY)) status |= SD_ROW_INVALID_DIST;
     }
 }
 
@@ -1257,6 +1278,12 @@ __device__ void finalize_write(const Plan& P, int b, const Decision& d, int64_t 
     if (P.d_keep)
         for (int s2 = P.n_tslots; s2 < P.slots; ++s2) status |= keep_of(P, b * P.slots + s2).flags;
     P.row_status[b] = status;
+    flag_error(P.status_or, status);
+    if (P.row_counts && (status & SD_ROW_DONE)) {   // one writer per row per call (stream-ordered calls)
+        int64_t* rc = P.row_counts + 2 * (int64_t)b;
+        rc[0] += d.n;
+        rc[1] += d.n + (d.mode != kModeNone && x >= 0 ? 1 : 0);
+    }
 }
 
 // STREAM mode: grid (B), one wave.
@@ -1550,7 +1577,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
                 if (poll_epoch) {   // poll mode: re-read until the record carries this call's tag (bounded)
                     const uint32_t tag = sample_tag(*poll_epoch, b, k);
                     for (int spin = 0; v.w != tag; ++spin) {
-                        if (spin >= (1 << 16)) { atomicOr(&s_xstat, SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST); break; }
+                        if (!spin_more(spin, P.spin_limit)) { atomicOr(&s_xstat, SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST); break; }
                         __builtin_amdgcn_s_sleep(1);
                         v = ld_coh16(rp + k);
                     }
@@ -1792,7 +1819,7 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
     const float2 ms = combine_row(P, r);
     if (lane == 0) {
         int32_t st = SD_ROW_DONE;
-        if (P.t_stoch && (!(ms.y > 0.f) || ms.y != ms.y)) st |= SD_ROW_INVALID_DIST;
+        if (P.t_stoch && !(ms.y > 0.f && ms.y < INFINITY)) st |= SD_ROW_INVALID_DIST;   // NaN / inf / zero mass
         if (P.t_keep) st |= keep_of(P, r).flags;
         if (P.noise.mode == SD_NOISE_STREAM && P.t_stoch && 2ll * P.V * P.B > P.noise.n_words)
             st |= SD_ROW_NOISE_OVERRUN;
@@ -1804,6 +1831,7 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
         }
         if (P.row_stats) P.row_stats[r] = ms;
         if (P.row_status) P.row_status[r] = st;
+        flag_error(P.status_or, st);
         if (P.keep_out && P.t_keep) P.keep_out[r] = keep_of(P, r);
         if (r == 0 && P.words_used) *P.words_used = P.t_stoch ? 2ll * P.V * P.B : 0;
     }
@@ -2016,6 +2044,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
         if (P.token_prob) P.token_prob[r] = x >= 0 ? prob_exact<DT>(l_y[cp], ms.x, ms.y, 1.0f / ms.y) : NAN;
         if (P.row_stats) P.row_stats[r] = ms;
         if (P.row_status) P.row_status[r] = st;
+        flag_error(P.status_or, st);
         if (P.keep_out && P.t_keep) P.keep_out[r] = keep_of(P, r);
         if (r == 0 && P.words_used) *P.words_used = 0;
     }
@@ -2051,6 +2080,8 @@ struct DrawLean {
     int32_t V, n_span;
     int32_t pstride;   // float4 partials per row: n_span rounded up to whole 128-B lines
     int32_t poll;      // 1: the row's last span polls tagged partials (no arrival counter)
+    int32_t spin_limit;   // bounded poll (sd_set_poll_policy)
+    int32_t* status_or;   // the caller's sticky error word (nullable)
 };
 
 // Poll-mode record tag: the row's epoch (counter set 2, advanced by the row's consumer after every
@@ -2278,15 +2309,17 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             rec[q] = make_uint4(0u, 0u, 0u, 0u);
         }
         for (int spin = 0;; ++spin) {
+            if (A.spin_limit >= 0) {   // < 0: the test hook, every record counts as lost
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                if (!have[q]) {
-                    rec[q] = ld_coh16(pr + 2 * (q * kWave + lane));
-                    have[q] = rec[q].w == draw_tag(epoch, r, q * kWave + lane, A.n_span);
+                for (int q = 0; q < 2; ++q) {
+                    if (!have[q]) {
+                        rec[q] = ld_coh16(pr + 2 * (q * kWave + lane));
+                        have[q] = rec[q].w == draw_tag(epoch, r, q * kWave + lane, A.n_span);
+                    }
                 }
+                if (__all(have[0] && have[1])) break;
             }
-            if (__all(have[0] && have[1])) break;
-            if (spin >= (1 << 16)) {   // bounded: ~tens of ms; the row is flagged, never a hang
+            if (!spin_more(spin, A.spin_limit)) {   // bounded: ~tens of ms; the row is flagged, never a hang
                 xstat = SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST;
                 break;
             }
@@ -2371,6 +2404,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             if (A.token_prob) A.token_prob[r] = x >= 0 ? bv : NAN;
             if (A.row_stats) A.row_stats[r] = make_float2(M, S);
             if (A.row_status) A.row_status[r] = st;
+            flag_error(A.status_or, st);
             if (r == 0 && A.words_used) *A.words_used = 0;
         }
         return;
@@ -2406,6 +2440,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         if (A.token_prob) A.token_prob[r] = x >= 0 ? prob_exact<DT>(yx, M, S, 1.0f / S) : NAN;
         if (A.row_stats) A.row_stats[r] = make_float2(M, S);
         if (A.row_status) A.row_status[r] = st;
+        flag_error(A.status_or, st);
         if (r == 0 && A.words_used) *A.words_used = 0;
     }
 }
@@ -2453,6 +2488,33 @@ __global__ void __launch_bounds__(kThreads) k_writeprobs(Plan P, void* out, int6
 // ====================================================================== host side
 namespace {
 thread_local hipError_t g_last_error = hipSuccess;
+
+// In-launch exchange policy (sd_set_poll_policy): whether poll-mode exchanges may be chosen at all,
+// and the bound of every poll.  Process-wide; SD_POLL / SD_POLL_SPIN_LIMIT set the initial values.
+constexpr int kDefaultSpin = 1 << 16;
+std::atomic<int> g_allow_poll{-1};
+std::atomic<int> g_spin_limit{kDefaultSpin};
+std::once_flag g_policy_once;
+void policy_init() {
+    std::call_once(g_policy_once, [] {
+        int allow = 1;
+        if (const char* e = getenv("SD_POLL")) allow = atoi(e) != 0;
+        int expected = -1;
+        g_allow_poll.compare_exchange_strong(expected, allow);
+        if (const char* e = getenv("SD_POLL_SPIN_LIMIT")) {
+            const int v = atoi(e);
+            g_spin_limit.store(v == 0 ? kDefaultSpin : v);
+        }
+    });
+}
+bool poll_allowed() {
+    policy_init();
+    return g_allow_poll.load(std::memory_order_relaxed) > 0;
+}
+int spin_limit() {
+    policy_init();
+    return g_spin_limit.load(std::memory_order_relaxed);
+}
 }  // namespace
 
 #include "sd_threshold.inc"
@@ -2581,7 +2643,7 @@ int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, in
 // once); SD_SAMPLE_POLL=0 keeps the arrival counters (A/B)
 bool sample_poll_ok(int B, const void* kern) {
     static const bool off = getenv("SD_SAMPLE_POLL") && atoi(getenv("SD_SAMPLE_POLL")) == 0;
-    if (off) return false;
+    if (off || !poll_allowed()) return false;
     static std::mutex mu;
     static std::map<std::pair<int, const void*>, int> caps;
     int dev = 0;
@@ -2731,7 +2793,9 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
         cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
     }
     static const bool no_poll = getenv("SD_DRAW_NO_POLL") != nullptr;   // A/B switch: counter mode only
-    A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && !no_poll;
+    A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && !no_poll && poll_allowed();
+    A.spin_limit = P.spin_limit;
+    A.status_or = P.status_or;
     SD_LAUNCH((k_draw_lean<DT, NST, GREEDY>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
     return SD_OK;
 }
@@ -2789,7 +2853,7 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
 int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* stream) {
     if (P.noise.mode != SD_NOISE_PHILOX || proc.kind != SD_PROC_NUCLEUS) return 0;
     if (!(proc.top_p >= sd::kNucMinP) || !(proc.temperature <= 1.f) || P.tdt == SD_F32) return 0;
-    if (P.token_prob || P.row_stats || P.keep_out) return 0;
+    if (P.token_prob || P.row_stats || P.keep_out || !poll_allowed()) return 0;
     if (const char* e = getenv("SD_NUC_REJECT"))
         if (!atoi(e)) return 0;
     // the verify's threshold search must cut this row with the same normaliser: its sub-slice mode
@@ -2822,6 +2886,8 @@ int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* strea
     A.V = P.V;
     A.T = proc.temperature;
     A.top_p = proc.top_p;
+    A.spin_limit = P.spin_limit;
+    A.status_or = P.status_or;
     const dim3 grid(nsl, P.B);
     if (P.tdt == SD_BF16)
         hipLaunchKernelGGL(sd::k_draw_nuc<SD_BF16>, grid, dim3(sd::kNucThreads), 0, (hipStream_t)stream, A);
@@ -2837,6 +2903,21 @@ int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* strea
 extern "C" {
 
 int32_t sd_abi_version(void) { return SD_ABI_VERSION; }
+
+int32_t sd_set_poll_policy(int32_t allow_poll, int32_t spin_limit_) {
+    if (allow_poll != 0 && allow_poll != 1) return SD_ERR_INVALID;
+    policy_init();
+    g_allow_poll.store(allow_poll);
+    g_spin_limit.store(spin_limit_ == 0 ? kDefaultSpin : spin_limit_);
+    return SD_OK;
+}
+
+int32_t sd_get_poll_policy(int32_t* allow_poll, int32_t* spin_limit_) {
+    if (!allow_poll || !spin_limit_) return SD_ERR_INVALID;
+    *allow_poll = poll_allowed() ? 1 : 0;
+    *spin_limit_ = spin_limit();
+    return SD_OK;
+}
 
 const char* sd_last_hip_error(void) { return hipGetErrorString(g_last_error); }
 
@@ -2904,6 +2985,9 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     P.stop_index = a->stop_index; P.row_status = a->row_status; P.words_used = a->words_used;
     P.generated = a->generated; P.gen_stride = a->generated_stride_b; P.step = a->step;
     P.finished = a->finished; P.accepted_count = a->accepted_count;
+    P.status_or = a->status_or;
+    P.row_counts = a->row_counts;
+    P.spin_limit = spin_limit();
     // drafter row stats that came with the draws (sd_sample row_stats): k_stats reads only the
     // target rows.  A top-k / nucleus drafter also needs the draws' keep predicates
     // (sd_sample row_keep): then the threshold search covers the target rows only.  Without
@@ -2985,6 +3069,8 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
     P.token_prob = a->token_prob; P.row_status = a->row_status; P.words_used = a->words_used;
     P.row_stats = reinterpret_cast<float2*>(a->row_stats);
     P.keep_out = reinterpret_cast<RowKeep*>(a->row_keep);
+    P.status_or = a->status_or;
+    P.spin_limit = spin_limit();
     set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);
@@ -3026,6 +3112,7 @@ int32_t sd_probs(const sd_probs_args* a, void* stream) {
     P.t_keep = needs_keep(a->proc);
     P.tT = a->proc.temperature; P.dT = 1.f;
     P.trow[0] = a->logits; P.tstride = a->stride_r;
+    P.spin_limit = spin_limit();
     set_stats_chunks(P, P.B);
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->rows, a->rows, 1, a->vocab);

@@ -13,9 +13,10 @@ Module layout mirrors the reference's import paths for the hot path:
 All compute goes through libspecdec.so (HIP, gfx950); importing fails if it is missing.
 """
 from . import _lib  # noqa: F401  (loads libspecdec.so or raises)
+from ._lib import RowError, get_poll_policy, set_poll_policy  # noqa: F401
 from .noise import PhiloxNoise, StreamNoise, default_noise, set_noise_mode  # noqa: F401
 from .ops import ProcSpec, proc_spec, probs_rows, sample_rows, verify  # noqa: F401
 from . import torch_ops  # noqa: F401,E402  (registers torch.ops.specdec.sample / .verify)
 
-__all__ = ["PhiloxNoise", "StreamNoise", "default_noise", "set_noise_mode", "ProcSpec", "proc_spec",
+__all__ = ["RowError", "get_poll_policy", "set_poll_policy", "PhiloxNoise", "StreamNoise", "default_noise", "set_noise_mode", "ProcSpec", "proc_spec",
            "probs_rows", "sample_rows", "verify"]

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 7
+SD_ABI_VERSION = 8
 SD_MAX_GAMMA = 16
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
@@ -28,6 +28,8 @@ SD_ROW_INVALID_DIST = 0x40
 SD_ROW_NOISE_OVERRUN = 0x80
 SD_ROW_NUCLEUS_INEXACT = 0x100
 SD_ROW_EXCHANGE_TIMEOUT = 0x200
+# the bits that make a row's outputs unusable (the reference raises there): status_or collects them
+SD_ROW_ERROR_MASK = SD_ROW_INVALID_DIST | SD_ROW_NOISE_OVERRUN | SD_ROW_EXCHANGE_TIMEOUT
 
 # SPECDEC_LIB selects another in-tree build of the same ABI (e.g. the phase-timing variant)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("SPECDEC_LIB", "libspecdec.so"))
@@ -39,7 +41,7 @@ EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify
            "sd_ngram_store_has_gram", "sd_ngram_store_draft",
            "sd_mt19937_state_from_torch", "sd_mt19937_state_to_torch", "sd_mt19937_jump_table",
            "sd_mt19937_char_poly", "sd_mt19937_fill_substreams", "sd_mt19937_generate_workspace_size",
-           "sd_mt19937_generate", "sd_mt19937_commit")
+           "sd_mt19937_generate", "sd_mt19937_commit", "sd_set_poll_policy", "sd_get_poll_policy")
 
 SD_MT_JUMP_WORDS = 320
 SD_MT_JUMP_CHUNKS = 16
@@ -99,6 +101,7 @@ class sd_verify_args(C.Structure):
         ("prof_stats_begin", C.c_void_p), ("prof_stats_end", C.c_void_p), ("prof_stats_repeat", C.c_int32),
         ("draft_row_stats", C.c_void_p), ("draft_row_stats_stride", C.c_int64),
         ("draft_row_keep", C.c_void_p),
+        ("status_or", C.c_void_p), ("row_counts", C.c_void_p),
     ]
 
 
@@ -110,6 +113,7 @@ class sd_sample_args(C.Structure):
         ("row_status", C.c_void_p), ("words_used", C.c_void_p),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
         ("row_stats", C.c_void_p), ("row_keep", C.c_void_p),
+        ("status_or", C.c_void_p),
     ]
 
 
@@ -133,6 +137,7 @@ class sd_ngram_args(C.Structure):
         ("stop_index", C.c_void_p), ("row_status", C.c_void_p), ("words_used", C.c_void_p),
         ("filler_ids", C.c_void_p), ("filler_stride_b", C.c_int64),
         ("workspace", C.c_void_p), ("workspace_bytes", C.c_size_t),
+        ("status_or", C.c_void_p),
     ]
 
 
@@ -195,6 +200,10 @@ def _load():
                                               C.c_void_p])):
         getattr(lib, name).restype = res
         getattr(lib, name).argtypes = args
+    lib.sd_set_poll_policy.restype = C.c_int32
+    lib.sd_set_poll_policy.argtypes = [C.c_int32, C.c_int32]
+    lib.sd_get_poll_policy.restype = C.c_int32
+    lib.sd_get_poll_policy.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     P = C.POINTER(sd_ngram_store)
     for name, args in (("sd_ngram_store_initialize", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_void_p]),
                        ("sd_ngram_store_update", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_int32,
@@ -224,3 +233,40 @@ def check(status: int, what: str):
         if status == SD_ERR_LAUNCH:
             msg += f": {lib.sd_last_hip_error().decode()}"
         raise SpecdecError(msg)
+
+
+def set_poll_policy(allow_poll: bool = True, spin_limit: int = 0) -> None:
+    """sd_set_poll_policy: whether kernels may exchange partials by polling inside one launch (the
+    occupancy check still decides per launch), and the bound of every poll (0 = default; < 0 gives
+    up at once — a test hook that forces the SD_ROW_EXCHANGE_TIMEOUT path)."""
+    check(lib.sd_set_poll_policy(1 if allow_poll else 0, int(spin_limit)), "sd_set_poll_policy")
+
+
+def get_poll_policy():
+    """(allow_poll, spin_limit) as the library holds them."""
+    a, s = C.c_int32(), C.c_int32()
+    check(lib.sd_get_poll_policy(C.byref(a), C.byref(s)), "sd_get_poll_policy")
+    return bool(a.value), int(s.value)
+
+
+class RowError(RuntimeError):
+    """A row's outputs are unusable (SD_ROW_ERROR_MASK): where the reference's torch.multinomial
+    raises (NaN / inf / all-zero probabilities, engine/infer_engine.py:246,321-325,
+    sampling/speculative_decoding.py:171), or an in-launch exchange timed out, or the STREAM noise
+    ran short.  The message is torch's for the invalid-distribution case."""
+
+
+def raise_row_error(bits: int, where: str) -> None:
+    """Raise RowError for the SD_ROW_ERROR_MASK bits of a row status / status_or word (no-op for 0)."""
+    bits = int(bits) & SD_ROW_ERROR_MASK
+    if not bits:
+        return
+    parts = []
+    if bits & SD_ROW_EXCHANGE_TIMEOUT:
+        parts.append("an in-launch exchange timed out (sd_set_poll_policy(allow_poll=False) selects the "
+                     "counter exchanges when other work shares the GPU)")
+    if bits & SD_ROW_NOISE_OVERRUN:
+        parts.append("the STREAM noise buffer ran short")
+    if bits & SD_ROW_INVALID_DIST and not bits & SD_ROW_EXCHANGE_TIMEOUT:
+        parts.append("probability tensor contains either `inf`, `nan` or element < 0")
+    raise RowError(f"{where}: " + "; ".join(parts) + f" (row status bits 0x{bits:x})")

@@ -8,10 +8,19 @@ depends on the whole batch, so the batch is tokenized once, identically on every
 ``batch_speculative_generate`` on it with ``ctx.row_base`` = its first global row, and the
 per-row outputs / rates / request metrics are gathered in global row order.
 
-Under Philox noise the draws are keyed by (seed, call offset, GLOBAL row), so the gathered
-outputs equal those of one process decoding the whole batch (tests/test_dp_engine_gpu.py).
-There is no collective on the data path: the one exchange is ``all_gather_object`` of the
-finished rows' host results.
+Noise: data parallelism is PHILOX-only.  Philox draws are keyed by (seed, call offset, GLOBAL row),
+so the gathered outputs equal those of one process decoding the whole batch
+(tests/test_gpu_engine_surface.py); after every batch the ranks agree on the call offset (the
+largest any rank reached — what one process, which runs until its last row finishes, would hold),
+so later batches stay equal too.  The bit-exact STREAM mode draws from ONE torch generator in the
+reference's serial row order (engine/infer_engine.py:280-330): independent ranks would each replay
+the same words, so ``batch_speculative_generate_dp`` refuses it (RuntimeError) rather than return
+outputs that match neither the reference nor one process.
+
+There is no collective on the data path: the exchanges are ``all_gather_object`` of the finished
+rows' host results and of the call offsets.  Ranks that share a GPU (more ranks than devices on a
+node) make the library's in-launch polls unsafe (a grid can be starved by another process's
+kernels), so the runner switches them off (``sd_set_poll_policy(allow_poll=0)``) when it sees that.
 """
 from __future__ import annotations
 
@@ -20,7 +29,8 @@ from typing import List, Optional, Tuple
 
 import torch
 
-from .. import dp
+from .. import _lib, dp
+from ..noise import PhiloxNoise, StreamNoise, default_noise
 from .batch_decode import decode_batch_with_chat_template
 from .infer_engine import _fill_batch_metrics, batch_speculative_generate
 from .metrics import BatchMetrics
@@ -41,14 +51,59 @@ def _gather(obj, dist):
     return out
 
 
+_SHARED_CHECKED = set()
+
+
+def ranks_share_devices(dist, device) -> bool:
+    """True when two ranks of `dist` run on the same GPU (same host, same device index)."""
+    world, _ = _world(dist)
+    if world == 1:
+        return False
+    import socket
+    dev = torch.device(device)
+    idx = dev.index if dev.index is not None else (torch.cuda.current_device() if dev.type == "cuda" else 0)
+    me = (socket.gethostname(), dev.type, idx)
+    everyone = _gather(me, dist)
+    return len(set(everyone)) < len(everyone)
+
+
+def configure_residency(dist, device) -> bool:
+    """Switch the library's in-launch polls off when ranks share a GPU (INTEGRATION.md
+    "Residency"): a poll-mode grid assumes it is alone on the device.  Checked once per process
+    group; returns whether polling stays allowed."""
+    key = id(dist) if dist is not None else None
+    if key not in _SHARED_CHECKED:
+        _SHARED_CHECKED.add(key)
+        if ranks_share_devices(dist, device):
+            _lib.set_poll_policy(allow_poll=False, spin_limit=_lib.get_poll_policy()[1])
+    return _lib.get_poll_policy()[0]
+
+
+def _sync_philox_offset(noise, dist) -> None:
+    """Every rank takes the largest call offset any rank reached: one process decoding the whole
+    batch runs until its LAST row finishes, so it holds that offset; ranks whose rows finished
+    earlier stopped calling sooner."""
+    world, _ = _world(dist)
+    if world == 1 or not isinstance(noise, PhiloxNoise):
+        return
+    noise.offset = max(_gather(int(noise.offset), dist))
+
+
 def batch_speculative_generate_dp(ctx, input_ids: torch.Tensor, attention_mask: torch.Tensor, dist=None,
                                   first_token_callback=None) -> Tuple[List[torch.Tensor], List[float], float]:
     """Decode the global batch [B, L] sharded over the ranks of `dist`.
 
     Returns (outputs, rates, elapsed) for the WHOLE batch on every rank (outputs on this rank's
     device, global row order) and this rank's decode wall time.  `first_token_callback` gets
-    GLOBAL row ids."""
+    GLOBAL row ids.  PHILOX noise only (module docstring): under the STREAM default every rank
+    raises RuntimeError before decoding anything."""
     world, rank = _world(dist)
+    noise = default_noise()
+    if world > 1 and isinstance(noise, StreamNoise):
+        raise RuntimeError("data-parallel decoding needs PHILOX noise (specdec_amd.set_noise_mode('philox')): "
+                           "the bit-exact STREAM mode draws every row from one torch generator in the "
+                           "reference's serial order, which independent ranks cannot share")
+    configure_residency(dist, input_ids.device)
     B = input_ids.shape[0]
     start, stop = dp.shard_rows(B, world, rank)
     saved = getattr(ctx, "row_base", None)
@@ -69,6 +124,7 @@ def batch_speculative_generate_dp(ctx, input_ids: torch.Tensor, attention_mask: 
         else:
             ctx.row_base = saved
     elapsed = time.time() - t0
+    _sync_philox_offset(noise, dist)
     shards = _gather((err, [o.cpu() for o in outs], rates), dist)
     errs = [s[0] for s in shards if s[0] is not None]
     if errs:

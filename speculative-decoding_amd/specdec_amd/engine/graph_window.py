@@ -67,11 +67,17 @@ class EngineWindow:
         self.cols = torch.arange(g, dtype=torch.long, device=dev)
         self.idx = torch.empty(g, dtype=torch.long, device=dev)
         self.all_done = torch.zeros(1, dtype=torch.uint8, device=dev)
+        # failed rows of every draw / verify (SD_ROW_ERROR_MASK), read with the finished flag
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.done_err = torch.zeros(2, dtype=torch.int32, device=dev)   # [all finished, err] per window
         self.o0 = noise.offset
         od = noise.offset_dev if noise.offset_dev is not None else torch.zeros(1, dtype=torch.long, device=dev)
         self.noise = PhiloxNoise(noise.seed, self.o0, od)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.windows_run = 0
+        self.on_window: Optional[Callable[[int], None]] = None   # host hook after window w is queued
+        self.first_draw_event: Optional[torch.cuda.Event] = None    # recorded after the first window's draw 0
+        self._first_recorded = False
 
     # ---------------------------------------------------------------- one window, device-only
     def _window(self, gw: int) -> None:
@@ -85,7 +91,12 @@ class EngineWindow:
         for d in range(gw):                              # :224-258
             logits = self.drafter_step(prev, d, self.step_dev)
             samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, self.noise, row_base=self.row_base,
-                                        row_stats_out=self.dstats[d])
+                                        row_stats_out=self.dstats[d], status_or=self.err)
+            samples.clamp_(min=0)                        # a failed row's -1 never reaches a forward
+            if d == 0 and self.first_draw_event is not None and not self._first_recorded \
+                    and not torch.cuda.is_current_stream_capturing():
+                self.first_draw_event.record()           # TTFT: the first draft of the first window
+                self._first_recorded = True
             torch.where(active, samples, torch.zeros_like(samples), out=self.win[:, d])   # :252,:257
             rows.append(logits)
             prev = self.win[:, d]
@@ -100,7 +111,7 @@ class EngineWindow:
         verify(trows, rows, win, _lib.SD_RULE_ENGINE, PLAIN_SOFTMAX, PLAIN_SOFTMAX, self.noise, self.stops,
                active=active.to(torch.uint8),
                engine_state=dict(generated=self.win, step=0, finished=self.finished, accepted=self.accepted),
-               row_base=self.row_base, draft_row_stats=self.dstats[:gw])
+               row_base=self.row_base, draft_row_stats=self.dstats[:gw], status_or=self.err)
         idx = self.idx[:gw]
         torch.add(self.cols[:gw], self.step_dev, out=idx)
         self.generated.index_copy_(1, idx, win)          # generated[:, step:step+gw] = window
@@ -108,6 +119,8 @@ class EngineWindow:
         self.step_dev.add_(gw)
         self.noise.advance_device(gw + 1)                # γ draws + 1 verify consumed
         self.all_done.copy_((self.finished != 0).all().to(torch.uint8).reshape(1))
+        self.done_err[0].copy_(self.all_done[0])
+        self.done_err[1].copy_(self.err[0])
 
     def capture(self) -> None:
         """Capture one full window.  Capturing records the launches without running them, so the
@@ -125,15 +138,18 @@ class EngineWindow:
         g = self.gamma
         lag = max(int(lag), 1)
         full, tail = divmod(self.gen_len, g)
-        flags = [torch.zeros(1, dtype=torch.uint8).pin_memory() for _ in range(lag)]
+        flags = [torch.zeros(2, dtype=torch.int32).pin_memory() for _ in range(lag)]
         events: List[Optional[torch.cuda.Event]] = [None] * lag
+        self.first_window_done: Optional[torch.cuda.Event] = None
 
-        def done_before(w: int) -> bool:   # the flag of window w - lag, if it ran
+        def done_before(w: int) -> bool:   # the flags of window w - lag, if it ran; a failed row raises
             ev = events[w % lag]
             if ev is None:
                 return False
             ev.synchronize()
-            return bool(flags[w % lag].item())
+            done, bits = flags[w % lag].tolist()
+            _lib.raise_row_error(bits, "EngineWindow")
+            return bool(done)
 
         for w in range(full):
             if done_before(w):                           # every row finished (:212)
@@ -145,11 +161,16 @@ class EngineWindow:
                     self.capture()
                 self.graph.replay()
             self.windows_run += 1
-            flags[w % lag].copy_(self.all_done, non_blocking=True)
+            flags[w % lag].copy_(self.done_err, non_blocking=True)
             events[w % lag] = torch.cuda.Event()
             events[w % lag].record()
+            if w == 0:
+                self.first_window_done = events[0]
+            if self.on_window is not None:
+                self.on_window(w)
         if tail:
             torch.cuda.current_stream(self.dev).synchronize()
+            _lib.raise_row_error(int(self.err.item()), "EngineWindow")
             if not bool(self.all_done.item()):
                 self._window(tail)
                 self.windows_run += 1

@@ -23,7 +23,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from .. import _lib
-from ..noise import PhiloxNoise, default_noise, noise_session
+from ..noise import PhiloxNoise, StreamNoise, default_noise, noise_session
 from ..ops import PLAIN_SOFTMAX, sample_rows, verify
 from .batch_decode import decode_batch_with_chat_template
 from .graph_window import EngineWindow
@@ -86,9 +86,10 @@ def run_batch_speculative(ctx, input_ids: torch.Tensor, attention_mask: torch.Te
     starts = [time.time()] * batch_size
     firsts: List[Optional[float]] = [None] * batch_size
 
-    def first_token(idx):
+    def first_token(idx, t=None):
         if idx < batch_size and firsts[idx] is None:
-            firsts[idx] = time.time()
+            firsts[idx] = time.time() if t is None else t
+    first_token.accepts_time = True   # the graph path reports the first draw's device completion time
 
     try:
         outputs, rates = batch_speculative_generate(ctx, input_ids, attention_mask, batch_size,
@@ -200,18 +201,38 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
     drafted = torch.zeros(B, dtype=torch.long, device=dev)
     accepted = torch.zeros(B, dtype=torch.long, device=dev)
     stops = torch.tensor(list(ctx.end_tokens), dtype=torch.long, device=dev)
+    # every draw's and every verify's failed rows (SD_ROW_ERROR_MASK) OR into one device word, read
+    # where the loop already syncs; set bits raise as torch.multinomial does in the reference
+    # (:246,321-325), and run_batch_speculative then returns None (:144-146)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
 
     if isinstance(noise, PhiloxNoise) and getattr(ctx, "drafter_step", None) is not None \
             and getattr(ctx, "target_rows", None) is not None:
         # capturable drafter / target steps: the whole window replays from one hipGraph (graph_window.py)
-        if first_token_callback is not None:
-            for idx in range(B):                                          # step 0: every row is active
-                first_token_callback(idx)
         win = EngineWindow(ctx.drafter_step, ctx.target_rows, input_ids[:, -1], gamma, gen_len, ctx.end_tokens,
                            noise, row_base=row_base)
-        win.run()
-        noise.offset = win.o0 + win.windows_run * (gamma + 1)             # the calls the windows consumed
-        return _collect(input_ids, win.generated, win.drafted, win.accepted, B)
+        # TTFT (:261-263: after step 0's first draft): the first draw's completion on the device,
+        # placed on the host clock by one event synchronised before the window is queued — no sync
+        # inside the loop.  A callback without a time argument is called after the run.
+        ref = torch.cuda.Event(enable_timing=True)
+        win.first_draw_event = torch.cuda.Event(enable_timing=True)
+        if first_token_callback is not None:
+            ref.record()
+            ref.synchronize()
+        t_ref = time.time()
+        try:
+            win.run()
+        finally:
+            noise.offset = win.o0 + win.windows_run * (gamma + 1)         # the calls the windows consumed
+        outs = _collect(input_ids, win.generated, win.drafted, win.accepted, B, win.err)
+        if first_token_callback is not None:
+            t_first = t_ref + ref.elapsed_time(win.first_draw_event) / 1e3
+            for idx in range(B):                                          # step 0: every row is active
+                if getattr(first_token_callback, "accepts_time", False):
+                    first_token_callback(idx, t_first)
+                else:
+                    first_token_callback(idx)
+        return outs
 
     # perf mode: each draw also returns its row's (max, Σexp), so verify reads only target rows
     stash = isinstance(noise, PhiloxNoise)
@@ -221,14 +242,17 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
     # the host queues the next window while the GPU runs this one.  A window over all-finished rows
     # changes nothing, so the outputs are the reference's.  STREAM keeps the exact check: such a
     # window would still consume generator words.
-    probe = _FinishedProbe(finished) if stash else None
+    probe = _FinishedProbe(finished, err) if stash else None
     step = 0
     while step < gen_len:                                                 # :211
         if probe is not None:
             if probe.done():
                 break
-        elif bool(finished.all()):
-            break
+        else:                                                             # one read: finished.all() and err
+            done, bits = torch.stack([(finished != 0).all().to(torch.int32), err[0]]).tolist()
+            _lib.raise_row_error(bits, "batch_speculative_generate")
+            if done:
+                break
         gw = min(gamma, gen_len - step)                                   # :216
         draft_tokens = torch.zeros(B, gw, dtype=torch.long, device=dev)
         active = finished == 0
@@ -241,8 +265,14 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
             out = ctx.drafter(prev.unsqueeze(1), past_key_values=past, use_cache=True)   # :239
             logits = out.logits[:, -1, :]
             past = out.past_key_values
+            if d == 0 and isinstance(noise, StreamNoise):
+                # the window's words in one generation: γ_w draws of 2·B·V, the verify's <= B·(γ_w + 2V)
+                V = logits.shape[-1]
+                noise.reserve(gw * 2 * B * V + B * (gw + 2 * V), dev)
             samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise,     # :241-246 softmax + multinomial
-                                        row_base=row_base, row_stats_out=dstats[d] if stash else None)
+                                        row_base=row_base, row_stats_out=dstats[d] if stash else None,
+                                        status_or=err)
+            samples.clamp_(min=0)   # a failed row's -1 (raised at the next read of err) never reaches a forward
             rows.append(logits)
             draft_tokens[:, d] = torch.where(active, samples, draft_tokens[:, d])          # :252
             generated[:, step + d] = torch.where(active, samples, generated[:, step + d])  # :257
@@ -259,25 +289,32 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
         verify(trows, rows, draft_tokens, _lib.SD_RULE_ENGINE, PLAIN_SOFTMAX, PLAIN_SOFTMAX, noise, stops,
                active=active.to(torch.uint8),
                engine_state=dict(generated=generated, step=step, finished=finished, accepted=accepted),
-               row_base=row_base, draft_row_stats=dstats[:gw] if stash and t_logits.device == dev else None)
+               row_base=row_base, draft_row_stats=dstats[:gw] if stash and t_logits.device == dev else None,
+               status_or=err)
         if probe is not None:
             probe.record()
         step += gw                                                        # :338
-    return _collect(input_ids, generated, drafted, accepted, B)
+    return _collect(input_ids, generated, drafted, accepted, B, err)
 
 
 class _FinishedProbe:
-    """finished.all() of the window before last, without a sync on the window just queued."""
+    """finished.all() and the error word of the window before last, without a sync on the window
+    just queued.  The lag costs at most one extra window after the last row finished (γ drafter
+    forwards and one target forward over rows that are all inactive: they draw nothing into the
+    outputs, so the tokens are the reference's; the Philox call offsets advance by that window's
+    γ + 1 calls).  A failed row raises one window late; its -1 tokens were clamped before any
+    forward saw them, and the batch's outputs are discarded with the exception."""
 
-    def __init__(self, finished: torch.Tensor):
-        self.finished = finished
-        self.flags = [torch.zeros(1, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    def __init__(self, finished: torch.Tensor, err: torch.Tensor):
+        self.finished, self.err = finished, err
+        self.flags = [torch.zeros(2, dtype=torch.int32).pin_memory() for _ in range(2)]
         self.events: List[Optional[torch.cuda.Event]] = [None, None]
         self.w = 0
 
     def record(self) -> None:
         i = self.w % 2
-        self.flags[i].copy_((self.finished != 0).all().to(torch.uint8).reshape(1), non_blocking=True)
+        both = torch.cat([(self.finished != 0).all().to(torch.int32).reshape(1), self.err])
+        self.flags[i].copy_(both, non_blocking=True)
         self.events[i] = torch.cuda.Event()
         self.events[i].record()
         self.w += 1
@@ -287,12 +324,18 @@ class _FinishedProbe:
         if ev is None:
             return False
         ev.synchronize()
-        return bool(self.flags[self.w % 2].item())
+        done, bits = self.flags[self.w % 2].tolist()
+        _lib.raise_row_error(bits, "batch_speculative_generate")
+        return bool(done)
 
 
-def _collect(input_ids, generated, drafted, accepted, B):
-    """engine/infer_engine.py:341-357: prompt + generated up to the last nonzero token, per-row rates."""
+def _collect(input_ids, generated, drafted, accepted, B, err=None):
+    """engine/infer_engine.py:341-357: prompt + generated up to the last nonzero token, per-row rates.
+    err: the loop's error word — a failed row raises here at the latest (torch raises in the
+    reference's loop, :246,321-325)."""
     dev = input_ids.device
+    if err is not None:
+        _lib.raise_row_error(int(err.item()), "batch_speculative_generate")
     gen_host = generated.cpu()
     drafted_h, accepted_h = drafted.tolist(), accepted.tolist()
     outputs, rates = [], []

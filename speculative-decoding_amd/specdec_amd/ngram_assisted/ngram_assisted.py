@@ -68,8 +68,9 @@ def ngram_assisted_speculative_generate(
     if first_target:                                              # :78-93 (no stop check here)
         ids_d = torch.tensor([ids], dtype=torch.long, device=dev)
         logits, cache, _ = _forward(target, ids_d, cur, cache, use_cache)
-        tok, _, _ = sample_rows(logits[:, -1, :], spec, noise)
-        t = int(tok[0].item())
+        tok, _, st = sample_rows(logits[:, -1, :], spec, noise)
+        t, bits = torch.stack([tok[0], st[0].long()]).tolist()
+        _lib.raise_row_error(bits, "ngram_assisted_speculative_generate")   # torch raises (:89-90)
         ids[prompt_len] = t
         cur += 1
         ngramstorage.update(as_2d(ids[:prompt_len]), as_2d([t]))
@@ -99,8 +100,7 @@ def ngram_assisted_speculative_generate(
                             out.stop_index[0].long()]).tolist()
         n, x, status, stop_index = (int(v) for v in head)
         fill = out.filler_ids[0].tolist() if filler else None
-        if status & _lib.SD_ROW_NOISE_OVERRUN:
-            raise RuntimeError("specdec: noise stream overrun")
+        _lib.raise_row_error(status, "ngram_assisted_speculative_generate")   # torch raises (:117,141)
         accepted += n
         if status & _lib.SD_ROW_STOP_IN_DRAFTS:                   # :126-131
             return drafted[prompt_len:cur + stop_index + 1], rate()

@@ -82,6 +82,7 @@ class _DeviceMT:
         return self.words[:n]
 
     def commit(self, count: Optional[int] = None, used_dev: Optional[torch.Tensor] = None) -> None:
+        """Move the state past `count` (host) + *used_dev (device) words of the last fill."""
         used_ptr = used_dev.data_ptr() if used_dev is not None else None
         _lib.check(lib.sd_mt19937_commit(self.state.data_ptr(), self.words.data_ptr(), self.n_generated, used_ptr,
                                          int(count or 0), None,
@@ -121,6 +122,7 @@ class StreamNoise:
         self.device_generation = _DEVICE_GEN if device_generation is None else bool(device_generation)
         self._dev: Optional[_DeviceMT] = None
         self._depth = 0
+        self._pool: Optional[Tuple[torch.Tensor, int]] = None   # (the reserved words, host cursor)
 
     @property
     def gen(self) -> torch.Generator:
@@ -143,24 +145,64 @@ class StreamNoise:
         self.gen.set_state(st)
 
     # ---- the kernels' interface (ops.py) -----------------------------------------------------
+    def _device_mt(self, dev: torch.device) -> _DeviceMT:
+        if self._dev is None or self._dev.device != dev:
+            if self._dev is not None:                   # moving devices mid-session: hand over
+                self._close_pool()
+                self._dev.pull(self.gen)
+            self._dev = _DeviceMT(dev, self.gen.get_state())
+        return self._dev
+
+    def reserve(self, n_words: int, device) -> None:
+        """Inside a session: generate the words of SEVERAL calls in one go — an engine window's γ
+        draws and its verify, whose word counts are known up front (2·B·V per draw, at most
+        B·(γ + 2V) for the verify).  One set of jump-ahead substreams and one generation launch
+        replace one per call; the calls then take consecutive slices (prepare) and the state is
+        committed once, by the host-known prefix plus the last call's device count.  No-op
+        outside a session or without device generation."""
+        dev = torch.device(device)
+        if self._depth == 0 or not self.device_generation or dev.type != "cuda":
+            return
+        self._close_pool()
+        words = self._device_mt(dev).fill(int(n_words))
+        self._pool = (words, 0)
+
+    def _close_pool(self, used_dev: Optional[torch.Tensor] = None) -> None:
+        """Commit a reserved pool by its host cursor (+ a device count) and drop it."""
+        if self._pool is None:
+            return
+        _, cursor = self._pool
+        self._pool = None
+        if cursor or used_dev is not None:
+            self._dev.commit(cursor, used_dev)
+
     def prepare(self, n_words: int, device) -> torch.Tensor:
         """Device words for a call that may consume up to n_words words."""
         dev = torch.device(device)
         if not self.device_generation or dev.type != "cuda":
             return self.draw(n_words, dev)
-        if self._dev is None or self._dev.device != dev:
-            if self._dev is not None:                   # moving devices mid-session: hand over
-                self._dev.pull(self.gen)
-            self._dev = _DeviceMT(dev, self.gen.get_state())
-        return self._dev.fill(n_words)
+        if self._pool is not None:
+            words, cursor = self._pool
+            if self._dev.device == dev and cursor + max(int(n_words), 1) <= words.numel() - 624:
+                return words[cursor:words.numel() - 624]   # the rest of the pool, minus the commit's slack
+            self._close_pool()                          # exhausted: commit what was used, fill anew
+        return self._device_mt(dev).fill(n_words)
 
     def consumed(self, count: Optional[int] = None, used_dev: Optional[torch.Tensor] = None) -> None:
         """The call consumed `count` words (or the device int64 `used_dev` holds the count)."""
         if self._dev is None:
             self.advance(int(used_dev.item()) if used_dev is not None else int(count or 0))
             return
-        self._dev.commit(count, used_dev)
+        if self._pool is not None:
+            words, cursor = self._pool
+            if used_dev is None:                        # a host-known count: the cursor moves
+                self._pool = (words, cursor + int(count or 0))
+            else:                                       # a device count ends the pool (its size is
+                self._close_pool(used_dev)              # unknown to the host until read)
+        else:
+            self._dev.commit(count, used_dev)
         if self._depth == 0:
+            self._close_pool()
             self._dev.pull(self.gen)
             self._dev = None
 
@@ -173,6 +215,7 @@ class StreamNoise:
         finally:
             self._depth -= 1
             if self._depth == 0 and self._dev is not None:
+                self._close_pool()
                 self._dev.pull(self.gen)
                 self._dev = None
 

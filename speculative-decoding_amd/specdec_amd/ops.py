@@ -109,6 +109,15 @@ def _require_rows(t: torch.Tensor, name: str, V: int) -> None:
         raise ValueError(f"{name}: unsupported dtype {t.dtype}")
 
 
+def _status_or_ptr(status_or: Optional[torch.Tensor], device):
+    """Device address of a caller's sticky error word (int32 [1] on the call's device), or None."""
+    if status_or is None:
+        return None
+    if status_or.dtype != torch.int32 or status_or.numel() < 1 or status_or.device != torch.device(device):
+        raise ValueError("status_or must be an int32 [1] tensor on the call's device")
+    return status_or.data_ptr()
+
+
 def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
     """(sd_noise, keepalive tensor) for a call that may consume up to n_words_needed words.
     row_base: global id of the call's row 0 (Philox noise is keyed by the global row)."""
@@ -129,7 +138,7 @@ def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
 # --------------------------------------------------------------------------- sampling
 def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Tensor] = None,
                 want_prob: bool = False, row_base: int = 0, row_stats_out: Optional[torch.Tensor] = None,
-                row_keep_out: Optional[torch.Tensor] = None):
+                row_keep_out: Optional[torch.Tensor] = None, status_or: Optional[torch.Tensor] = None):
     """LogitsProcessor.__call__ + .sample on every row of logits [R, V] (one sample per row).
 
     Returns (tokens int64 [R], token_prob fp32 [R] or None, row_status int32 [R]).  Under
@@ -141,6 +150,8 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     row's keep predicate (sd_row_keep: tau as fp32 bits, tie index, flags) — what
     ``verify(draft_row_keep=...)`` takes with the stats so the verify skips the drafter rows'
     threshold search.  Not written for other processors.
+    status_or: optional int32 [1] device word; every row's SD_ROW_ERROR_MASK bits are ORed into it
+    (the decode loops test it where they already sync instead of reading every row_status).
     """
     spec = proc_spec(proc)
     R, V = logits.shape
@@ -166,7 +177,8 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
                             prob.data_ptr() if prob is not None else None, status.data_ptr(), None,
                             ws.data_ptr(), ws.numel(),
                             row_stats_out.data_ptr() if row_stats_out is not None else None,
-                            row_keep_out.data_ptr() if row_keep_out is not None else None)
+                            row_keep_out.data_ptr() if row_keep_out is not None else None,
+                            _status_or_ptr(status_or, dev))
     _lib.check(lib.sd_sample(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_sample")
     if isinstance(noise, StreamNoise):
         noise.consumed(count=need)
@@ -210,7 +222,9 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
            active: Optional[torch.Tensor] = None, engine_state: Optional[dict] = None,
            sync_noise: bool = True, prof_events=None, row_base: int = 0,
            draft_row_stats: Optional[torch.Tensor] = None,
-           draft_row_keep: Optional[torch.Tensor] = None) -> VerifyOut:
+           draft_row_keep: Optional[torch.Tensor] = None,
+           status_or: Optional[torch.Tensor] = None,
+           row_counts: Optional[torch.Tensor] = None) -> VerifyOut:
     """One verify step for B sequences.
 
     target_rows: γ+1 (SPEC) or γ (ENGINE) tensors [B, V] — row t of every sequence;
@@ -226,6 +240,9 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
     draft_row_keep: optional int32 [γ, S, 4] device tensor at draft_row_stats' row layout — the
     drafter rows' keep predicates as ``sample_rows(row_keep_out=...)`` returned them; the
     threshold search then covers the target rows only.
+    status_or: optional int32 [1] device word that collects every row's SD_ROW_ERROR_MASK bits.
+    row_counts: optional int64 [B, 2] contiguous device tensor; each call ADDS (accepted drafts,
+    tokens emitted) to every row's pair (the A12 bookkeeping, kept on the device).
     """
     gamma = len(draft_rows)
     if not 1 <= gamma <= _lib.SD_MAX_GAMMA:
@@ -318,6 +335,12 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         a.draft_row_stats, a.draft_row_stats_stride = draft_row_stats.data_ptr(), draft_row_stats.stride(0) // 2
     if draft_row_keep is not None:
         a.draft_row_keep = draft_row_keep.data_ptr()
+    a.status_or = _status_or_ptr(status_or, dev)
+    if row_counts is not None:
+        if row_counts.dtype != torch.long or tuple(row_counts.shape) != (B, 2) or not row_counts.is_contiguous() \
+                or row_counts.device != dev:
+            raise ValueError(f"row_counts must be a contiguous int64 [{B}, 2] tensor on {dev}")
+        a.row_counts = row_counts.data_ptr()
     if prof_events is not None:   # (torch.cuda.Event, torch.cuda.Event[, repeats]) around the row-stats kernel
         a.prof_stats_begin, a.prof_stats_end = prof_events[0].cuda_event, prof_events[1].cuda_event
         a.prof_stats_repeat = int(prof_events[2]) if len(prof_events) > 2 else 1
@@ -342,7 +365,7 @@ class NgramOut:
 
 def ngram_verify(target_rows: Sequence[torch.Tensor], draft_tokens: Optional[torch.Tensor], proc, noise,
                  stop_tokens: Optional[torch.Tensor] = None, filler_k: int = 0, sync_noise: bool = True,
-                 row_base: int = 0) -> NgramOut:
+                 row_base: int = 0, status_or: Optional[torch.Tensor] = None) -> NgramOut:
     """ngram_assisted/ngram_assisted.py:111-164 verify step for B sequences.
 
     target_rows: γ'+1 tensors [B, V] — rows 0..γ'-1 verify drafts 0..γ'-1, row γ' is the bonus row;
@@ -393,6 +416,7 @@ def ngram_verify(target_rows: Sequence[torch.Tensor], draft_tokens: Optional[tor
     a.filler_ids = out.filler_ids.data_ptr() if filler_k else None
     a.filler_stride_b = (gamma + 1) * filler_k
     a.workspace, a.workspace_bytes = ws.data_ptr(), ws.numel()
+    a.status_or = _status_or_ptr(status_or, dev)
     _lib.check(lib.sd_ngram_verify(C.byref(a), C.c_void_p(_stream_ptr(dev))), "sd_ngram_verify")
     if isinstance(noise, StreamNoise) and sync_noise:
         noise.consumed(used_dev=out.words_used)

@@ -20,7 +20,7 @@ import torch
 from torch.nn import Module
 
 from .. import _lib
-from ..noise import PhiloxNoise, default_noise, noise_session
+from ..noise import PhiloxNoise, StreamNoise, default_noise, noise_session
 from ..ops import proc_spec, sample_rows, verify
 from ..utils.caching import prune_cache
 from ..utils.logits_processor import GreedyProcessor, LogitsProcessor
@@ -115,12 +115,24 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
     dlen = tlen = 0                                              # host copies of the static lengths
     if static:
         drafter_cache, target_cache = _static_caches(drafter, target, total_len)
+    # every draw's and verify's failed rows (SD_ROW_ERROR_MASK) OR into one device word, read with the
+    # integers each step already reads back: where torch.multinomial raises in the reference
+    # (:96,123,171), this loop raises too — a draw's -1 is clamped to 0 first, so no forward ever
+    # indexes an embedding with it before the error is seen
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    err_d = err if torch.device(drafter.device) == torch.device(dev) else \
+        torch.zeros(1, dtype=torch.int32, device=drafter.device)
+
+    def check_err():
+        bits = int(err.item()) | (int(err_d.item()) if err_d is not err else 0)
+        _lib.raise_row_error(bits, "speculative_generate")
 
     if first_target:                                             # :84-103
         logits, target_cache, _ = _forward(target, input_ids, cur, target_cache, use_cache, tlen if static else None)
         tlen = cur
-        sample_rows(logits[:, -1, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1])
-        t = int(input_ids[0, cur].item())
+        sample_rows(logits[:, -1, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1], status_or=err)
+        t, bits = torch.stack([input_ids[0, cur], err[0].long()]).tolist()
+        _lib.raise_row_error(bits, "speculative_generate")
         cur += 1
         if t in stops:
             return input_ids[0, prompt_len:cur].tolist(), 0
@@ -140,8 +152,13 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
                                                 dlen if static else None)
             dlen = cur + k
             row = logits[:, -1, :]
-            sample_rows(row, spec, noise, tokens_out=ids_d[0, cur + k:cur + k + 1],
-                        row_stats_out=dstats[k] if stash else None)
+            if k == 0 and isinstance(noise, StreamNoise) and spec.stochastic and row.device == torch.device(dev):
+                # the step's words in one generation: g draws of 2V, the verify's g + 2V
+                V = row.shape[-1]
+                noise.reserve(g * 2 * V + g + 2 * V, dev)
+            tok = ids_d[0, cur + k:cur + k + 1]
+            sample_rows(row, spec, noise, tokens_out=tok, row_stats_out=dstats[k] if stash else None, status_or=err_d)
+            tok.clamp_(min=0)
             draft_rows.append(row if row.device == torch.device(dev) else row.to(dev))
         drafts_speculated += g
         input_ids = ids_d.to(dev)
@@ -150,7 +167,9 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         tlen = cur + g
         if g == 0:
             # last position: rand(0) draws nothing, n = 0 = γ', the bonus row is sampled (:158-171)
-            sample_rows(logits[:, cur - 1 - start, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1])
+            sample_rows(logits[:, cur - 1 - start, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1],
+                        status_or=err)
+            check_err()
             x = int(input_ids[0, cur].item())
             cur += 1
             if x in stops:
@@ -159,13 +178,13 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         trows = [logits[:, cur - 1 + t - start, :] for t in range(g + 1)]   # :135 and bonus row :159
         out = verify(trows, draft_rows, input_ids[:, cur:cur + g], _lib.SD_RULE_SPEC, spec, spec, noise,
                      stop_t, skip_sample_adjustment=skip_sample_adjustment,
-                     draft_row_stats=dstats[:g] if stash else None)
-        n, x, status, stop_index = (int(v) for v in torch.stack([
-            out.n_accepted[0].long(), out.next_token[0], out.row_status[0].long(), out.stop_index[0].long()]).tolist())
-        if status & _lib.SD_ROW_INVALID_DIST:
-            raise RuntimeError("probability tensor contains either `inf`, `nan` or element < 0")
-        if status & _lib.SD_ROW_NOISE_OVERRUN:
-            raise RuntimeError("specdec: noise stream overrun")
+                     draft_row_stats=dstats[:g] if stash else None, status_or=err)
+        if err_d is not err:
+            err.bitwise_or_(err_d.to(dev))
+        n, x, status, stop_index, bits = (int(v) for v in torch.stack([
+            out.n_accepted[0].long(), out.next_token[0], out.row_status[0].long(), out.stop_index[0].long(),
+            err[0].long()]).tolist())
+        _lib.raise_row_error(bits | status, "speculative_generate")   # a draft draw's or this verify's
         drafts_accepted += n                                     # :147
         if status & _lib.SD_ROW_STOP_IN_DRAFTS:                  # :150-155
             return input_ids[0, prompt_len:cur + stop_index + 1].tolist(), drafts_accepted / drafts_speculated

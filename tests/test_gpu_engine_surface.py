@@ -6,7 +6,9 @@
   the BatchMetrics feed BenchmarkResults.to_dict;
 * the data-parallel runner (specdec_amd.engine.dp_runner): two processes (gloo, both on cuda:0 —
   the GPU box has one card) decoding row shards of one batch under Philox noise return exactly
-  what one process decoding the whole batch returns.
+  what one process decoding the whole batch returns, for two batches in a row (the call offsets
+  are agreed after each); STREAM noise is refused; ranks sharing the card run with the
+  library's in-launch polls switched off (the counter exchanges).
 """
 import json
 import os
@@ -74,14 +76,25 @@ def _dp_worker(rank, world, port, seed, out):
         torch.cuda.set_device(0)
         from specdec_amd import set_noise_mode
         from specdec_amd.engine.dp_runner import batch_speculative_generate_dp, run_batch_speculative_dp
+        from specdec_amd import get_poll_policy
         ctx, ids = _decode_setup()
+        # STREAM (the bit-exact default) is refused: independent ranks cannot share one generator
+        set_noise_mode("stream")
+        try:
+            batch_speculative_generate_dp(ctx, ids, torch.ones_like(ids), dist)
+            refused = False
+        except RuntimeError:
+            refused = True
         set_noise_mode("philox", seed=seed)
         outs, rates, _ = batch_speculative_generate_dp(ctx, ids, torch.ones_like(ids), dist)
+        # a second batch without re-seeding: the ranks agreed on the call offset after the first
+        outs2, _, _ = batch_speculative_generate_dp(ctx, ids.flip(0), torch.ones_like(ids), dist)
         set_noise_mode("philox", seed=seed)
         bm = run_batch_speculative_dp(ctx, ids, torch.ones_like(ids), ids.shape[0], dist)
         if rank == 0:
             out.put(([o.cpu().tolist() for o in outs], rates,
-                     [(r.generated_tokens, r.acceptance_rate) for r in bm.requests]))
+                     [(r.generated_tokens, r.acceptance_rate) for r in bm.requests],
+                     [o.cpu().tolist() for o in outs2], refused, get_poll_policy()[0]))
     finally:
         dist.destroy_process_group()
 
@@ -94,6 +107,8 @@ def test_dp_runner_two_ranks_equal_one_process():
     set_noise_mode("philox", seed=seed)
     want, wrates = batch_speculative_generate(ctx, ids, torch.ones_like(ids), ids.shape[0])
     want = [o.cpu().tolist() for o in want]
+    want2, _ = batch_speculative_generate(ctx, ids.flip(0), torch.ones_like(ids), ids.shape[0])
+    want2 = [o.cpu().tolist() for o in want2]
     set_noise_mode("stream")
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
@@ -101,10 +116,13 @@ def test_dp_runner_two_ranks_equal_one_process():
     procs = [mpc.Process(target=_dp_worker, args=(r, 2, port, seed, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got, rates, reqs = q.get(timeout=180)
+    got, rates, reqs, got2, refused, polled = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
     assert got == want and rates == wrates
+    assert got2 == want2            # the second batch too: the ranks' Philox call offsets agree
+    assert refused                  # DP under STREAM noise raises
+    assert polled is False          # both ranks on cuda:0: the runner switched in-launch polls off
     assert [g for g, _ in reqs] == [len(o) - ids.shape[1] for o in want]
     assert [a for _, a in reqs] == wrates
