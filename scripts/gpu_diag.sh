@@ -1,7 +1,8 @@
 #!/bin/bash
-# GPU-box recipe: perf-mode tests + phase timing + short bench (outputs under gpurun_out/)
+# GPU-box diagnostics of the STREAM path: the mt19937 round microbenchmark and the phase timelines
+# of k_rowsample / k_walk (timing build).  Outputs under gpurun_out/.
 set -eo pipefail
-cd $GRAFT_REPO_ROOT
-timeout -k 10 300 python -m pytest tests/test_gpu_perfmode.py -q -m gpu -x -s > gpurun_out/gpu_perf_tests.log 2>&1
-timeout -k 10 200 python scripts/phase_timing.py > gpurun_out/phase.log 2>&1
-timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err
+R=$GRAFT_REPO_ROOT
+cd $R
+timeout -k 10 120 ./scripts/microbench/mt_gen_bench > gpurun_out/mt_gen_bench.txt 2>&1
+timeout -k 10 120 python scripts/stream_phases.py > gpurun_out/stream_phases.txt 2>&1

@@ -18,7 +18,7 @@ from specdec_amd import noise as nz  # noqa: E402
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 2 * 32 * 128256
 g = torch.Generator().manual_seed(1)
 for stride in (16384, 32768, 65536, 131072):
-    nz.MT_STRIDE = stride
+    nz.MT_STRIDE, nz._STRIDE_ENV = stride, str(stride)
     d = nz._DeviceMT("cuda", g.get_state())
     t0 = time.perf_counter()
     d.fill(n)

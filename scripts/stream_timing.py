@@ -26,4 +26,5 @@ with noise.session():
     for _ in range(n):
         step()
     torch.cuda.synchronize()
-    print(f"STREAM engine step B={B}: {(time.perf_counter() - t0) / n * 1e3:.3f} ms")
+    from specdec_amd import noise as nz
+    print(f"STREAM engine step B={B} stride={nz.mt_stride(step.g * 2 * B * V + B * (step.g + 2 * V))}: {(time.perf_counter() - t0) / n * 1e3:.3f} ms")

@@ -35,6 +35,15 @@ constexpr int kBaseLen = kN + 1 + kJBits + 640 + 15;       // 21760: covers tau0
 constexpr int kRing = 2048;
 constexpr int kK = 10;                                     // window words per lane in k_mt_jump
 
+// A workgroup barrier for LDS hand-offs only.  __syncthreads() also orders the threads' GLOBAL
+// stores at workgroup scope, i.e. waits for every output store of the round to be acknowledged
+// (vmcnt(0)) before the barrier — ~1000 cycles per recurrence round in k_mt_gen, whose rounds only
+// exchange words through LDS.  Here: LDS operations complete (lgkmcnt(0)), then s_barrier; the
+// "memory" clobber keeps the compiler from moving memory accesses across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ uint32_t mag(uint32_t a, uint32_t b) {
     const uint32_t y = (a & 0x80000000u) | (b & 0x7fffffffu);
     return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
@@ -60,32 +69,65 @@ __device__ __forceinline__ uint32_t untemper(uint32_t y) {
     return t;
 }
 
-// ---------------------------------------------------------------------------------------- base
-__global__ void __launch_bounds__(256) k_mt_base(const sd_mt_state* __restrict__ st, uint32_t* __restrict__ base) {
-    __shared__ uint32_t ring[kRing];
+// ---------------------------------------------------------------------------------- recurrence
+// Unrolling the recurrence three times,
+//     x[q] = x[q-681] ^ F(q-1078) ^ F(q-851) ^ F(q-624),      F(p) = mag(x[p], x[p+1]),
+// every input of position q is at least 623 positions back: the 623 positions of a round are
+// independent, one barrier per round (the plain recurrence makes 454 per barrier, two of them
+// chained in each thread).  The LDS ring is double-mapped — x[q] at r[q & 2047] and
+// r[(q & 2047) + 2048] — so a round's seven reads are one base address plus immediate offsets.
+// Reads cover [q0 - 1078, q0), writes [q0, q0 + 623): disjoint modulo 2048, hence one barrier.
+constexpr int kBlk = kN - 1;           // 623 positions per round
+constexpr int kMtThreads = 640;        // 10 waves: a round's 623 positions, one per thread
+constexpr int kBack = 1078;            // the oldest input of a round, q - 1078
+
+__device__ __forceinline__ void ring_put(uint32_t* r, int64_t q, uint32_t x) {
+    const int i = (int)(q & (kRing - 1));
+    r[i] = x;
+    r[i + kRing] = x;
+}
+
+// Extend the ring holding x[0 .. 624) to x[len), calling out(q, x) for q in [624, len).  Whole
+// workgroup of kMtThreads; the caller put x[0 .. 624) in the ring and synchronised.
+template <typename Out>
+__device__ __forceinline__ void mt_extend(uint32_t* r, int64_t len, Out out) {
     const int t = threadIdx.x;
-    for (int j = t; j < kN; j += 256) {
-        const uint32_t w = st->mt[j];
-        ring[j] = w;
-        base[j] = w;
+    // [624, 1078): the plain recurrence, one round of two chained positions per thread
+    if (t < kLag) {
+        const int q1 = kN + t, q2 = q1 + kLag;
+        const uint32_t x1 = r[kM + t] ^ mag(r[t], r[t + 1]);
+        const uint32_t x2 = x1 ^ mag(r[q2 - kN], r[q2 - kN + 1]);
+        ring_put(r, q1, x1);
+        ring_put(r, q2, x2);
+        out(q1, x1);
+        out(q2, x2);
+    }
+    lds_barrier();
+    for (int64_t q0 = kBack; q0 < len; q0 += kBlk) {
+        if (t < kBlk) {
+            const int64_t q = q0 + t;
+            const uint32_t* b = r + (int)(q & (kRing - 1)) + kRing - kBack;   // b[k] = x[q - 1078 + k]
+            const uint32_t x = b[397] ^ mag(b[0], b[1]) ^ mag(b[227], b[228]) ^ mag(b[454], b[455]);
+            ring_put(r, q, x);
+            out(q, x);
+        }
+        lds_barrier();
+    }
+}
+
+// ---------------------------------------------------------------------------------------- base
+__global__ void __launch_bounds__(kMtThreads) k_mt_base(const sd_mt_state* __restrict__ st, uint32_t* __restrict__ base) {
+    __shared__ uint32_t ring[2 * kRing];
+    const int t = threadIdx.x;
+    if (t < kN) {
+        const uint32_t w = st->mt[t];
+        ring_put(ring, t, w);
+        base[t] = w;
     }
     __syncthreads();
-    // epoch: thread t < 227 makes q1 = q0 + t and q2 = q1 + 227; q - 227 is the thread's own
-    // previous word, q - 624 and q - 623 were made before the last barrier
-    uint32_t prev = t < kLag ? ring[kM + t] : 0u;          // x[q1 - 227] for the first epoch
-    for (int q0 = kN; q0 < kBaseLen; q0 += 2 * kLag) {
-        if (t < kLag) {
-            const int q1 = q0 + t, q2 = q1 + kLag;
-            const uint32_t x1 = prev ^ mag(ring[(q1 - kN) & (kRing - 1)], ring[(q1 - kN + 1) & (kRing - 1)]);
-            const uint32_t x2 = x1 ^ mag(ring[(q2 - kN) & (kRing - 1)], ring[(q2 - kN + 1) & (kRing - 1)]);
-            ring[q1 & (kRing - 1)] = x1;
-            ring[q2 & (kRing - 1)] = x2;
-            if (q1 < kBaseLen) base[q1] = x1;
-            if (q2 < kBaseLen) base[q2] = x2;
-            prev = x2;
-        }
-        __syncthreads();
-    }
+    mt_extend(ring, kBaseLen, [&](int64_t q, uint32_t x) {
+        if (q < kBaseLen) base[q] = x;
+    });
 }
 
 // ---------------------------------------------------------------------------------------- jump
@@ -134,41 +176,30 @@ __global__ void __launch_bounds__(64) k_mt_jump(const sd_mt_state* __restrict__ 
 }
 
 // ----------------------------------------------------------------------------------------- gen
-__global__ void __launch_bounds__(256) k_mt_gen(const sd_mt_state* __restrict__ st, const uint32_t* __restrict__ base,
-                                                const uint32_t* __restrict__ partial, int nch, uint32_t* __restrict__ out,
-                                                int64_t n, int64_t stride) {
-    __shared__ uint32_t ring[kRing];
+__global__ void __launch_bounds__(kMtThreads) k_mt_gen(const sd_mt_state* __restrict__ st, const uint32_t* __restrict__ base,
+                                                       const uint32_t* __restrict__ partial, int nch, uint32_t* __restrict__ out,
+                                                       int64_t n, int64_t stride) {
+    __shared__ uint32_t ring[2 * kRing];
     const int s = blockIdx.x, t = threadIdx.x;
     const int64_t lo = (int64_t)s * stride;
     const int64_t len = n - lo < stride ? n - lo : stride;
     uint32_t* o = out + lo;
-    for (int j = t; j < kN; j += 256) {
+    if (t < kN) {
         uint32_t w;
         if (s == 0) {
-            w = base[st->tau0 + j];
+            w = base[st->tau0 + t];
         } else {
             w = 0u;
-            const uint32_t* p = partial + (size_t)(s - 1) * nch * kN + j;
+            const uint32_t* p = partial + (size_t)(s - 1) * nch * kN + t;
             for (int c = 0; c < nch; ++c) w ^= p[(size_t)c * kN];
         }
-        ring[j] = w;
-        if (j < len) o[j] = temper(w);
+        ring_put(ring, t, w);
+        if (t < len) o[t] = temper(w);
     }
     __syncthreads();
-    uint32_t prev = t < kLag ? ring[kM + t] : 0u;
-    for (int64_t q0 = kN; q0 < len; q0 += 2 * kLag) {
-        if (t < kLag) {
-            const int64_t q1 = q0 + t, q2 = q1 + kLag;
-            const uint32_t x1 = prev ^ mag(ring[(q1 - kN) & (kRing - 1)], ring[(q1 - kN + 1) & (kRing - 1)]);
-            const uint32_t x2 = x1 ^ mag(ring[(q2 - kN) & (kRing - 1)], ring[(q2 - kN + 1) & (kRing - 1)]);
-            ring[q1 & (kRing - 1)] = x1;
-            ring[q2 & (kRing - 1)] = x2;
-            if (q1 < len) o[q1] = temper(x1);
-            if (q2 < len) o[q2] = temper(x2);
-            prev = x2;
-        }
-        __syncthreads();
-    }
+    mt_extend(ring, len, [&](int64_t q, uint32_t x) {
+        if (q < len) o[q] = temper(x);
+    });
 }
 
 // -------------------------------------------------------------------------------------- commit
@@ -221,14 +252,14 @@ int32_t sd_mt19937_generate(const sd_mt_generate_args* a, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     uint32_t* base = (uint32_t*)a->workspace;
     uint32_t* partial = (uint32_t*)((char*)a->workspace + (((size_t)kBaseLen * 4 + 255) & ~(size_t)255));
-    hipLaunchKernelGGL(k_mt_base, dim3(1), dim3(256), 0, s, a->state, base);
+    hipLaunchKernelGGL(k_mt_base, dim3(1), dim3(kMtThreads), 0, s, a->state, base);
     if (!launch_ok()) return SD_ERR_LAUNCH;
     if (S > 1) {
         hipLaunchKernelGGL((k_mt_jump<kJBits / SD_MT_JUMP_CHUNKS>), dim3(SD_MT_JUMP_CHUNKS, (unsigned)(S - 1)), dim3(64),
                            0, s, a->state, base, a->jump_table, partial);
         if (!launch_ok()) return SD_ERR_LAUNCH;
     }
-    hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)S), dim3(256), 0, s, a->state, base, partial, SD_MT_JUMP_CHUNKS,
+    hipLaunchKernelGGL(k_mt_gen, dim3((unsigned)S), dim3(kMtThreads), 0, s, a->state, base, partial, SD_MT_JUMP_CHUNKS,
                        a->words, a->n_words, a->stride_words);
     return launch_ok() ? SD_OK : SD_ERR_LAUNCH;
 }

@@ -458,6 +458,51 @@ __device__ __forceinline__ float exp1_from_words(uint32_t hi, uint32_t lo) {  //
     return (float)(-log1p(-u));
 }
 
+// The same Exp(1) value in fp32 arithmetic, for SCREENING only (relative error <= 2^-21 against
+// exp1_from_words): u < 1/2 as -log1p(-u) with u rounded to fp32 (log1p stays well conditioned),
+// u >= 1/2 as -log(1 - u) with 1 - u formed exactly in integers and rounded once.  The kernels
+// find the few elements that can win an exponential race with it, and evaluate only those with
+// the exact fp64 form — so torch's values decide the race, at fp32 cost per element.
+constexpr float kExpFastRelErr = 4.76837158203125e-07f;   // 2^-21
+__device__ __forceinline__ float exp1_fast_from_words(uint32_t hi, uint32_t lo) {
+    const uint64_t v = ((((uint64_t)hi) << 32) | lo) & ((1ull << 53) - 1);
+    if (v < (1ull << 52)) return -log1pf(-(float)v * 1.1102230246251565e-16f);
+    return -__logf((float)((1ull << 53) - v) * 1.1102230246251565e-16f);
+}
+
+// A cheaper screening value for 16-bit rows (relative error <= 2^-11 against exp1_from_words; the
+// races over bf16 / fp16 values tolerate far more): u < 2^-10 as u (1 + u/2), u < 1/2 as
+// -ln(1 - u) with 1 - u rounded once in fp32, u >= 1/2 as -ln of 1 - u formed from the words with
+// one rounding; v_log_f32 for the logarithm.  About ten VALU instructions, no branches.
+constexpr float kExpScreen16RelErr = 4.8828125e-04f;   // 2^-11
+__device__ __forceinline__ float exp1_screen16(uint32_t hi, uint32_t lo) {
+    const uint32_t h = hi & 0x1FFFFFu;                  // the top 21 of the 53 bits
+    const float lof = (float)lo * 1.1102230246251565e-16f;   // lo * 2^-53
+    const float u = fmaf((float)h, 4.76837158203125e-07f, lof);                    // h * 2^-21 + lo * 2^-53
+    const float w = h < (1u << 20) ? 1.0f - u : fmaf((float)((1u << 21) - h), 4.76837158203125e-07f, -lof);
+    const float big = -__builtin_amdgcn_logf(w) * 0.693147180559945309f;            // -ln(w)
+    return u < 9.765625e-04f ? u * fmaf(0.5f, u, 1.0f) : big;
+}
+
+// torch's exponential_ words of VEC consecutive elements (two per element, from woff + 2 e0): 16-byte
+// loads when aligned and in range, else per-word loads; words past the buffer read as 0 (the
+// callers flag the overrun).
+template <int VEC>
+__device__ __forceinline__ void stream_words(const sd_noise& nz, int64_t woff, int64_t e0, uint32_t* w) {
+    const int64_t w0 = woff + 2 * e0;
+    const uint32_t* src = nz.words + w0;
+    if (w0 + 2 * VEC <= nz.n_words && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+#pragma unroll
+        for (int q = 0; q < VEC / 2; ++q) {
+            const uint4 t = reinterpret_cast<const uint4*>(src)[q];
+            w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 2 * VEC; ++k) w[k] = w0 + k < nz.n_words ? src[k] : 0u;
+    }
+}
+
 // Philox4x32-10 (Salmon et al., SC'11), counter-based: perf-mode noise.
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint2 k) {
 #pragma unroll

@@ -769,45 +769,118 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
     return used;
 }
 
+// STREAM k_walk's LDS budget: the uniform windows of a block of rows (words), and the block's
+// per-draft inputs (rows x gamma)
+constexpr int kWalkWords = 12288;
+constexpr int kWalkDrafts = 1024;
+
 __global__ void __launch_bounds__(256) k_walk(Plan P) {
     if (P.noise.mode == SD_NOISE_STREAM) {
-        // The reference draws row after row from one generator: the rows' word offsets form a serial
-        // chain.  One wave walks it, each row in one round trip: lane i loads draft i's uniform (at
-        // the row's offset), its p/q and its drafted id together and tests it; lane 0 walks the
-        // flags (walk_core's rules) and moves the offset.
-        __shared__ uint8_t lacc[SD_MAX_GAMMA], lstop[SD_MAX_GAMMA];
-        if (threadIdx.x >= kWave) return;
-        const int lane = threadIdx.x, g = P.gamma;
-        int64_t off = 0;
-        for (int b = 0; b < P.B; ++b) {
-            bool acc = false, stop = false, ovr = false;
-            if (lane < g) {
-                const int64_t w = off + lane;
-                ovr = w >= P.noise.n_words;
-                const float u = ovr ? 0.f : uniform_from_word(P.noise.words[w]);
-                acc = accept_draft(P, P.rp[b * g + lane], P.rq[b * g + lane], u);
-                stop = is_stop(P, P.draft_tokens[b * P.tok_stride + lane]);
-            }
-            const uint64_t accm = __ballot(acc), stopm = __ballot(stop), ovrm = __ballot(ovr);
-            int64_t next = off;
-            if (lane == 0) {
-                for (int i = 0; i < g; ++i) {
-                    lacc[i] = (uint8_t)((accm >> i) & 1u);
-                    lstop[i] = (uint8_t)((stopm >> i) & 1u);
+        // The reference draws row after row from one generator (engine/infer_engine.py:280-330;
+        // sampling/speculative_decoding.py:139-171): the rows' word offsets form a serial chain.
+        // Row b's words start at off + a + 2V k, where a counts the uniforms the earlier rows of the
+        // block drew (<= g per row) and k the Exp(1) rows they drew (<= 1 per row).  So every
+        // uniform a block of nb rows can read lies in nb windows [off + 2V k, off + 2V k + nb g).
+        //   1. the workgroup loads those windows, and the block's accept thresholds (fp64 min(1,p/q)
+        //      / fp32 p/q, divided in parallel), stop and active flags, into LDS: one round trip;
+        //   2. wave 0 walks the chain from LDS — a row per step, its drafts on the lanes (one LDS
+        //      load and two ballots per row), only the offsets (a, k) carried;
+        //   3. every row's decision is rebuilt from its (a, k) and published in parallel.
+        // (Before: one dependent global round trip per row, ~3 us each.)
+        __shared__ uint32_t lw[kWalkWords];
+        __shared__ double lthr[kWalkDrafts];
+        __shared__ float lrp[kWalkDrafts], lrq[kWalkDrafts];
+        __shared__ uint8_t lstop[kWalkDrafts], lact[kWalkDrafts];
+        __shared__ int32_t la[kWalkDrafts], lk[kWalkDrafts];
+        __shared__ int64_t s_off;
+        const int tid = threadIdx.x, lane = tid & 63, g = P.gamma;
+        const int64_t V2 = 2ll * P.V;
+        const bool spec = P.rule == SD_RULE_SPEC;
+        int nbmax = 1;
+        while ((nbmax + 1) * (nbmax + 1) * g <= kWalkWords && (nbmax + 1) * g <= kWalkDrafts) ++nbmax;
+        if (tid == 0) s_off = 0;
+        SD_TS(8000, 0);
+        __syncthreads();
+        for (int b0 = 0; b0 < P.B; b0 += nbmax) {
+            const int nb = min(nbmax, P.B - b0), W = nb * g;
+            const int64_t off = s_off;
+            {   // every load in flight before the first LDS write (a loop of load -> store pairs waited
+                // for each load in turn: ~16 dependent round trips)
+                constexpr int kPer = kWalkWords / 256;
+                uint32_t wv[kPer];
+#pragma unroll
+                for (int q = 0; q < kPer; ++q) {
+                    const int i = tid + q * 256;
+                    const int k = i / W, j = i - k * W;
+                    const int64_t w = off + V2 * k + j;
+                    wv[q] = i < nb * W && w < P.noise.n_words ? P.noise.words[w] : 0u;
                 }
-                int64_t used;
-                Decision d = walk_core(P, b, P.rp + b * g, P.rq + b * g, off, &used, lacc, lstop);
-                // the uniforms come first in a row's words: SPEC reads all γ', ENGINE one per tested draft
-                const int64_t n_u = P.rule == SD_RULE_SPEC ? g : (d.mode == kModeResid ? used - 2ll * P.V : used);
-                const uint64_t umask = n_u >= 64 ? ~0ull : ((1ull << n_u) - 1ull);
-                if (ovrm & umask) d.status |= SD_ROW_NOISE_OVERRUN;
-                publish_decision(P, b, d);
-                next = off + used;
+#pragma unroll
+                for (int q = 0; q < kPer; ++q)
+                    if (tid + q * 256 < nb * W) lw[tid + q * 256] = wv[q];
             }
-            off = ((int64_t)__builtin_amdgcn_readlane((int)(next >> 32), 0) << 32) |
-                  (uint32_t)__builtin_amdgcn_readlane((int)(next & 0xffffffff), 0);
+            for (int i = tid; i < W; i += blockDim.x) {
+                const int b = b0 + i / g, d = i - (i / g) * g;
+                const float p = P.rp[b * g + d], q = P.rq[b * g + d];
+                lrp[i] = p;
+                lrq[i] = q;
+                // accept iff u <= p/q (fp32, SPEC) / u < min(1, p/q) (fp64, ENGINE): accept_draft's rules
+                lthr[i] = spec ? (double)(p / q) : ((double)q <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)q));
+                lstop[i] = is_stop(P, P.draft_tokens[b * P.tok_stride + d]) ? 1 : 0;
+                lact[i] = P.active == nullptr || P.active[b] != 0;
+            }
+            __syncthreads();
+            SD_TS(8000, 1);
+            if (tid < kWave) {   // the chain: (a, k) of every row
+                int a = 0, k = 0;
+                const bool in = lane < g;
+                for (int bi = 0; bi < nb; ++bi) {
+                    if (lane == 0) { la[bi] = a; lk[bi] = k; }
+                    const int e = bi * g + (in ? lane : 0);
+                    const float u = uniform_from_word(lw[k * W + a + (in ? lane : 0)]);
+                    const double t = lthr[e];
+                    const bool acc = spec ? !((double)u > t) : (double)u < t;
+                    const uint64_t rej = __ballot(in && !acc), stp = __ballot(in && lstop[e] != 0);
+                    const int f = rej ? __builtin_ctzll(rej) : g;              // first rejected draft
+                    const uint64_t before = f >= 64 ? ~0ull : ((1ull << f) - 1ull);
+                    const uint64_t stop_acc = stp & before;
+                    if (spec) {
+                        a += g;
+                        k += (P.t_stoch && !stop_acc) ? 1 : 0;
+                    } else if (lact[bi * g] != 0) {
+                        if (stop_acc) a += __builtin_ctzll(stop_acc) + 1;      // finished on an end token
+                        else if (f < g) { a += f + 1; k += 1; }                  // rejected: the residual row
+                        else a += g;
+                    }
+                }
+                if (lane == 0) s_off = off + a + V2 * k;
+            }
+            __syncthreads();
+            SD_TS(8000, 2);
+            // every row's decision from its offsets (walk_core's rules), published in parallel
+            for (int bi = tid; bi < nb; bi += blockDim.x) {
+                const int b = b0 + bi;
+                const int64_t woff = off + la[bi] + V2 * lk[bi];
+                uint8_t lacc[SD_MAX_GAMMA];
+                bool ovr = false;
+                int64_t used;
+#pragma unroll
+                for (int i = 0; i < SD_MAX_GAMMA; ++i) {
+                    if (i >= g) break;
+                    const float u = uniform_from_word(lw[lk[bi] * W + la[bi] + i]);
+                    lacc[i] = (spec ? !((double)u > lthr[bi * g + i]) : (double)u < lthr[bi * g + i]) ? 1 : 0;
+                }
+                Decision d = walk_core(P, b, lrp + bi * g, lrq + bi * g, woff, &used, lacc, lstop + bi * g);
+                const bool sampled = spec ? (d.mode != kModeNone && P.t_stoch) : d.mode == kModeResid;
+                const int64_t n_u = used - (sampled ? V2 : 0);
+                for (int i = 0; i < n_u; ++i) ovr |= woff + i >= P.noise.n_words;
+                if (ovr) d.status |= SD_ROW_NOISE_OVERRUN;
+                publish_decision(P, b, d);
+            }
+            __syncthreads();
+            SD_TS(8000, 3);
         }
-        if (lane == 0 && P.words_used) *P.words_used = off;
+        if (tid == 0 && P.words_used) *P.words_used = s_off;
     } else {
         for (int b = threadIdx.x; b < P.B; b += blockDim.x) walk_seq(P, b, 0);
         if (threadIdx.x == 0 && P.words_used) *P.words_used = 0;
@@ -988,10 +1061,77 @@ __global__ void __launch_bounds__(kThreads) k_decide_perf(Plan P) {
     decide_seq(P, b, pf, 8192 - 1 - b);
 }
 
+// STREAM exponential race of one chunk: the exact argmax (first index on ties) of
+// round_dt(p_j / round_dt(E_j)), p_j = round_dt(exp(y_j - M) / S) the processed probability and
+// E_j torch's exponential_ value from words woff + 2j (exp1_from_words, fp64 log1p).  Screened in
+// fp32: a_j = p'_j / E'_j with a cheap E' and, for 16-bit rows, the unrounded p' = e^(y_j - M)
+// (the common 1/S drops out of the comparison).  The exact values differ from a_j by at most the
+// dt roundings and the screening errors, so every element that can be the chunk's exact maximum
+// has a_j >= max_chunk(a) (1 - tol); only those take the exact path.  Whole workgroup; returns the
+// chunk's (value, index) in pv / pi.
+template <int DT>
+__device__ __forceinline__ float race_tol() {
+    // tol >= 4.2 u_dt + 2 (screening errors of p and E); about twice that, for margin
+    return DT == SD_BF16 ? 0.0625f : (DT == SD_F16 ? 0.0078125f : 7.62939453125e-06f);
+}
+template <int DT, int EPT>
+__device__ __forceinline__ void stream_race(const sd_noise& nz, int64_t woff, const float* y, const bool* ok,
+                                            const uint32_t* wd, const int64_t* jj, float M, float S, float invS,
+                                            float& pv, int32_t& pi, float* ldsf, int32_t* ldsi) {
+    float a[EPT];
+    float am = 0.f;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        const bool inw = woff + 2 * jj[k] + 1 < nz.n_words;
+        float e, p;
+        if constexpr (DT == SD_F32) {
+            e = exp1_fast_from_words(wd[2 * k], wd[2 * k + 1]);
+            p = prob_exact<DT>(y[k], M, S, invS);
+        } else {
+            e = exp1_screen16(wd[2 * k], wd[2 * k + 1]);
+            p = __builtin_amdgcn_exp2f((y[k] - M) * kLog2e);
+        }
+        a[k] = ok[k] ? p * __builtin_amdgcn_rcpf(inw ? e : 1.f) : -INFINITY;
+        am = fmaxf(am, a[k]);
+    }
+    const float bm = block_reduce(am, FMax(), ldsf);
+    const float thr = bm * (1.0f - race_tol<DT>());
+    pv = -INFINITY;
+    pi = INT_MAX;
+    // candidates; an all-zero chunk keeps each thread's first element (exact value 0)
+    uint32_t cm = 0;
+    bool first = true;
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+        if (!ok[k]) continue;
+        if (a[k] >= thr && (a[k] > 0.f || first)) cm |= 1u << k;
+        first = false;
+    }
+    // the exact values, one candidate at a time (one copy of the fp64 code; registers selected by
+    // an unrolled compare so nothing is indexed dynamically)
+    while (cm) {
+        const int k = __builtin_ctz(cm);
+        cm &= cm - 1u;
+        float yk = 0.f;
+        uint32_t h = 0u, l = 0u;
+        int64_t j = 0;
+#pragma unroll
+        for (int kk = 0; kk < EPT; ++kk)
+            if (kk == k) { yk = y[kk]; h = wd[2 * kk]; l = wd[2 * kk + 1]; j = jj[kk]; }
+        const float pk = prob_exact<DT>(yk, M, S, invS);
+        const float eb = round_dt<DT>(woff + 2 * j + 1 < nz.n_words ? exp1_from_words(h, l) : 1.f);
+        const float val = div_round<DT>(pk, eb, __builtin_amdgcn_rcpf(eb));
+        if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
+    }
+    block_argmax(pv, pi, ldsf, ldsi);
+}
+
 // ------------------------------------------------------------------ k_resample
 // grid (chunk, B).  RESID: Σ(p_n - q_n)+ and the argmax candidates of fl(fl(res/S)/E) in one pass
 // over the two rows; BONUS / PROW: argmax of the multinomial (or greedy) value of the target row.
-constexpr float kCandTol = 1.0f - 16.0f * 5.9604645e-08f;   // candidates within 16 ulp of the max
+// candidates within 64 ulp of the max: the roundings of fl(fl(res/S)/E) (<= a few ulp) and, under
+// STREAM noise, the fp32 screening value of E (exp1_fast_from_words, <= 8 ulp, on both sides)
+constexpr float kCandTol = 1.0f - 64.0f * 5.9604645e-08f;
 
 template <int TDT, int DDT, int NZ, int EPT, bool FAST>
 __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float2 mst, float2 msd_in) {
@@ -1022,13 +1162,26 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
 
     float sum = 0.f, wmax = 0.f;
     float res[EPT], ev[EPT];
+    // STREAM: the words stay in registers; ev holds the fp32 screening value of E, and the exact
+    // value is formed for the candidates only
+    uint32_t wd[NZ == SD_NOISE_STREAM ? 2 * EPT : 1];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
         float xt[VEC], xd[VEC], e[VEC];
         load_vecn<TDT, VEC>(trow, e0, P.V, t_al, xt);
         load_vecn<DDT, VEC>(drow, e0, P.V, d_al, xd);   // draft_is_probs dispatches DDT = F32
-        if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
+        if constexpr (NZ == SD_NOISE_STREAM) {
+            if (stoch) {
+                stream_words<VEC>(P.noise, d.noise_off, e0, wd + 2 * v * VEC);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k)
+                    e[k] = d.noise_off + 2 * (e0 + k) + 1 < P.noise.n_words
+                               ? exp1_fast_from_words(wd[2 * (v * VEC + k)], wd[2 * (v * VEC + k) + 1]) : 1.f;
+            }
+        } else {
+            if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
+        }
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
@@ -1056,21 +1209,35 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
     // any j whose exact fl(fl(res/S)/E) can tie the maximum has res/E within a few ulp of it
     const float thr = bw * kCandTol;
     if (bw > 0.f) {
+        uint32_t cm = 0;
 #pragma unroll
-        for (int v = 0; v < NV; ++v)
+        for (int idx = 0; idx < EPT; ++idx) {
+            const float w = stoch ? res[idx] * __builtin_amdgcn_rcpf(ev[idx]) : res[idx];
+            if (res[idx] > 0.f && w >= thr) cm |= 1u << idx;
+        }
+        while (cm) {   // one candidate at a time (registers selected by an unrolled compare)
+            const int idx = __builtin_ctz(cm);
+            cm &= cm - 1u;
+            float rr = 0.f, ee = 1.f;
+            uint32_t h = 0u, l = 0u;
 #pragma unroll
-            for (int k = 0; k < VEC; ++k) {
-                const int idx = v * VEC + k;
-                const float w = stoch ? res[idx] * __builtin_amdgcn_rcpf(ev[idx]) : res[idx];
-                if (res[idx] > 0.f && w >= thr) {
-                    const int slot = atomicAdd(&lcount, 1);
-                    if (slot < kMaxCand) {
-                        lres[slot] = res[idx];
-                        le[slot] = ev[idx];
-                        lidx[slot] = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k);
-                    }
+            for (int kk = 0; kk < EPT; ++kk)
+                if (kk == idx) {
+                    rr = res[kk];
+                    ee = ev[kk];
+                    if constexpr (NZ == SD_NOISE_STREAM) { h = wd[2 * kk]; l = wd[2 * kk + 1]; }
                 }
+            const int v = idx / VEC, k = idx - v * VEC;
+            const int64_t j = base + ((int64_t)v * kThreads + threadIdx.x) * VEC + k;
+            const int slot = atomicAdd(&lcount, 1);
+            if (slot < kMaxCand) {
+                if constexpr (NZ == SD_NOISE_STREAM)   // the exact value, for the candidates only
+                    if (stoch) ee = d.noise_off + 2 * j + 1 < P.noise.n_words ? exp1_from_words(h, l) : 1.f;
+                lres[slot] = rr;
+                le[slot] = ee;
+                lidx[slot] = (int32_t)j;
             }
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1100,6 +1267,35 @@ __device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2
     const float t_inv = 1.0f / mst.y;
     float pv = -INFINITY;
     int32_t pi = INT_MAX;
+    if constexpr (NZ == SD_NOISE_STREAM) {
+        if (stoch) {   // the screened exponential race (stream_race)
+            float pr[EPT];
+            uint32_t wd[2 * EPT];
+            int64_t jj[EPT];
+            bool ok[EPT];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+                float xt[VEC];
+                load_vec<TDT>(trow, e0, P.V, t_al, xt);
+                stream_words<VEC>(P.noise, d.noise_off, e0, wd + 2 * v * VEC);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) {
+                    const int64_t j = e0 + k;
+                    jj[v * VEC + k] = j;
+                    ok[v * VEC + k] = j < P.V;
+                    pr[v * VEC + k] = FAST ? xt[k] : process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt);   // y
+                }
+            }
+            stream_race<TDT, EPT>(P.noise, d.noise_off, pr, ok, wd, jj, mst.x, mst.y, t_inv, pv, pi, ldsf, ldsi);
+            if (threadIdx.x == 0) {
+                ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
+                st_coh(&o.pval, pv);
+                st_coh(&o.pidx, pi);
+            }
+            return;
+        }
+    }
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
@@ -1756,12 +1952,60 @@ __global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
 
 // ------------------------------------------------------------------ sd_sample kernels
 // grid (chunk, R): argmax of round_dt(p / round_dt(E)) (multinomial) or p (greedy).
-template <int DT, int NZ, int EPT>
+template <int DT, int NZ, int EPT, bool FAST = false>
 __device__ void rowsample_body(const Plan& P, int r, int c) {
     __shared__ float ldsf[8];
     __shared__ int32_t ldsi[8];
     __shared__ float2 lms;
     constexpr int VEC = Elem<DT>::kVec, NV = EPT / VEC;
+    if constexpr (NZ == SD_NOISE_STREAM) {
+        if (P.t_stoch) {
+            // the chunk's logits and noise words are loaded first (independent of the row stats),
+            // then the stats, then the screened race
+            const int ts_wg = r * P.rn_chunks + c;
+            SD_TS(ts_wg, 0);
+            const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (DT == SD_F32 ? 4 : 2);
+            const bool al = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
+            const int64_t base = (int64_t)c * P.rchunk;
+            const int64_t woff = 2ll * P.V * r;
+            float x[EPT];
+            uint32_t wd[2 * EPT];
+            int64_t jj[EPT];
+            bool ok[EPT];
+#pragma unroll
+            for (int v = 0; v < NV; ++v) {
+                const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+                load_vec<DT>(row, e0, P.V, al, x + v * VEC);
+                stream_words<VEC>(P.noise, woff, e0, wd + 2 * v * VEC);
+#pragma unroll
+                for (int k = 0; k < VEC; ++k) { jj[v * VEC + k] = e0 + k; ok[v * VEC + k] = e0 + k < P.V; }
+            }
+            if (threadIdx.x < 64) {
+                const float2 ms = combine_row(P, r);
+                if (threadIdx.x == 0) lms = ms;
+            }
+            __syncthreads();
+            SD_TS(ts_wg, 1);
+            const float2 ms = lms;
+            const float inv_s = 1.0f / ms.y;
+            if (!FAST) {   // the processed values y (T, top-k / nucleus mask)
+                const RowKeep kp = P.t_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
+#pragma unroll
+                for (int k = 0; k < EPT; ++k) x[k] = process_value<DT>(x[k], jj[k], P.tT, P.t_keep, kp);
+            }
+            SD_TS(ts_wg, 2);
+            float pv;
+            int32_t pi;
+            stream_race<DT, EPT>(P.noise, woff, x, ok, wd, jj, ms.x, ms.y, inv_s, pv, pi, ldsf, ldsi);
+            SD_TS(ts_wg, 3);
+            if (threadIdx.x == 0) {
+                ResPart& o = P.rpart[(int64_t)r * P.rn_chunks + c];
+                o.pval = pv;
+                o.pidx = pi;
+            }
+            return;
+        }
+    }
     if (threadIdx.x < 64) {
         const float2 ms = combine_row(P, r);
         if (threadIdx.x == 0) lms = ms;
@@ -1803,9 +2047,9 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
     }
 }
 
-template <int DT, int NZ, int EPT>
+template <int DT, int NZ, int EPT, bool FAST = false>
 __global__ void __launch_bounds__(kThreads) k_rowsample(Plan P) {
-    rowsample_body<DT, NZ, EPT>(P, blockIdx.y, blockIdx.x);
+    rowsample_body<DT, NZ, EPT, FAST>(P, blockIdx.y, blockIdx.x);
 }
 
 __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
@@ -2082,7 +2326,22 @@ struct DrawLean {
     int32_t poll;      // 1: the row's last span polls tagged partials (no arrival counter)
     int32_t spin_limit;   // bounded poll (sd_set_poll_policy)
     int32_t* status_or;   // the caller's sticky error word (nullable)
+    int32_t affine;       // rows % 8 == 0: every span of a row on one XCD group (affine_split)
+    uint64_t* ts;         // phase timestamps (SD_PHASE_TIMING builds only)
 };
+
+// phase timestamps of k_draw_lean (diagnostic builds): slot wg = r * n_span + c
+#ifdef SD_PHASE_TIMING
+#define SD_TSL(wg, ph)                                                                                 \
+    do {                                                                                               \
+        if (threadIdx.x == 0 && A.ts) A.ts[(size_t)(wg) * 16 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define SD_TSL(wg, ph) \
+    do {               \
+        (void)(wg);    \
+    } while (0)
+#endif
 
 // Poll-mode record tag: the row's epoch (counter set 2, advanced by the row's consumer after every
 // draw) hashed with the row, the span and the span count.  Every row advances its epoch in step,
@@ -2133,8 +2392,11 @@ __device__ int greedy_rescan(const DrawLean& A, const char* row, int c, float M,
 template <int DT, int NST, bool GREEDY = false>
 __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     constexpr int VEC = 8, STEP = kThreads * VEC, EPT = NST * VEC, NW = kThreads / kWave;
-    const int c = blockIdx.x, r = blockIdx.y;
+    int c = blockIdx.x, r = blockIdx.y;
+    if (A.affine) affine_split(blockIdx.y * gridDim.x + blockIdx.x, (int)gridDim.x, r, c);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int ts_wg = r * A.n_span + c;
+    SD_TSL(ts_wg, 0);
     const char* row = A.rows + (int64_t)r * A.stride_bytes;
     const int64_t base = (int64_t)c * NST * STEP;
     float y[EPT];
@@ -2174,6 +2436,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
 #pragma unroll
     for (int k = 1; k < EPT; ++k) mv = fmaxf(mv, y[k]);
     const float mw = wave_max(mv);
+    SD_TSL(ts_wg, 1);
     float wv[EPT];
     float tl = 0.f;
 #pragma unroll
@@ -2246,6 +2509,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         }
     }
     __syncthreads();
+    SD_TSL(ts_wg, 2);
     if (w != 0) return;
     const bool bad = T != T;   // NaN / +inf in the span: S_c NaN flags the row
     const float m_pub = bad && !(m > -INFINITY) ? 0.f : m, s_pub = bad ? NAN : T;
@@ -2275,6 +2539,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
                 const uint32_t gd = GREEDY && g_dirty ? 0x8000u : 0u;
                 st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), off | gd | (yraw << 16), tag));
             }
+            SD_TSL(ts_wg, 3);
             return;
         }
     } else {
@@ -2325,6 +2590,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
+        SD_TSL(ts_wg, 4);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int k = q * kWave + lane;
@@ -2443,6 +2709,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         flag_error(A.status_or, st);
         if (r == 0 && A.words_used) *A.words_used = 0;
     }
+    SD_TSL(ts_wg, 5);
 }
 
 // ------------------------------------------------------------------ sd_probs kernel
@@ -2725,8 +2992,14 @@ int32_t launch_resample(const sd::Plan& P, void* stream) {
 template <int DT>
 int32_t launch_rowsample_dt(const sd::Plan& P, void* stream) {
     const dim3 grid(P.rn_chunks, P.B);
-    if (P.noise.mode == SD_NOISE_STREAM) SD_LAUNCH((k_rowsample<DT, SD_NOISE_STREAM, 8>), grid, dim3(kThreads), stream, P);
-    else SD_LAUNCH((k_rowsample<DT, SD_NOISE_PHILOX, 8>), grid, dim3(kThreads), stream, P);
+    // FAST: T = 1 and no top-k / nucleus mask (the engine's plain softmax draws)
+    const bool fast = P.tT == 1.0f && !P.t_keep;
+    if (P.noise.mode == SD_NOISE_STREAM) {
+        if (fast) SD_LAUNCH((k_rowsample<DT, SD_NOISE_STREAM, 8, true>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_rowsample<DT, SD_NOISE_STREAM, 8>), grid, dim3(kThreads), stream, P);
+    } else {
+        SD_LAUNCH((k_rowsample<DT, SD_NOISE_PHILOX, 8>), grid, dim3(kThreads), stream, P);
+    }
     return SD_OK;
 }
 
@@ -2796,6 +3069,10 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
     A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && !no_poll && poll_allowed();
     A.spin_limit = P.spin_limit;
     A.status_or = P.status_or;
+    A.ts = P.ts;
+    // XCD-affine placement (a row's spans and its poll exchange on one XCD group): SD_DRAW_AFFINE=1
+    static const int affine_env = getenv("SD_DRAW_AFFINE") ? atoi(getenv("SD_DRAW_AFFINE")) : 0;
+    A.affine = affine_env && P.B % 8 == 0;
     SD_LAUNCH((k_draw_lean<DT, NST, GREEDY>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
     return SD_OK;
 }

@@ -28,7 +28,22 @@ from ._lib import lib
 
 
 _DEVICE_GEN = os.environ.get("SPECDEC_STREAM_DEVICE", "1") != "0"
-MT_STRIDE = int(os.environ.get("SPECDEC_MT_STRIDE", "65536"))   # words per device substream
+# Words per device substream.  Jump-ahead cost grows with the number of substreams (~0.33 us each),
+# generation time with their length (one workgroup per substream, ~0.47 ns per word), and a
+# substream per CU at most keeps every generation round uncontended (a CU running two is
+# VALU-bound: 487 vs 292 ns per round, profiles/r3b_mt_gen_bench.txt).  So the stride is the
+# smallest multiple of 64 Ki words that needs at most kMaxSubstreams substreams (an engine step's
+# 41 M words at B = 32, V = 128256: 192 Ki words, 209 substreams).  SPECDEC_MT_STRIDE pins it.
+_STRIDE_ENV = os.environ.get("SPECDEC_MT_STRIDE")
+MT_STRIDE = int(_STRIDE_ENV) if _STRIDE_ENV else 65536
+MT_MAX_SUBSTREAMS = 240
+
+
+def mt_stride(n_words: int) -> int:
+    if _STRIDE_ENV:
+        return MT_STRIDE
+    per = -(-int(n_words) // MT_MAX_SUBSTREAMS)
+    return max(MT_STRIDE, -(-per // 65536) * 65536)
 _JUMP: Dict[Tuple[torch.device, int], torch.Tensor] = {}
 
 
@@ -69,12 +84,13 @@ class _DeviceMT:
         n = max(int(n_words), 1) + 624
         if self.words.numel() < n:
             self.words = torch.empty(n + n // 4, dtype=torch.int32, device=self.device)
-        S = (n + MT_STRIDE - 1) // MT_STRIDE
-        table = jump_table(self.device, MT_STRIDE, max(S - 1, 1))
-        need = lib.sd_mt19937_generate_workspace_size(n, MT_STRIDE)
+        stride = mt_stride(n)
+        S = (n + stride - 1) // stride
+        table = jump_table(self.device, stride, max(S - 1, 1))
+        need = lib.sd_mt19937_generate_workspace_size(n, stride)
         if self.ws.numel() < need:
             self.ws = torch.empty(need + need // 4, dtype=torch.uint8, device=self.device)
-        a = _lib.sd_mt_generate_args(self.state.data_ptr(), table.data_ptr(), table.shape[0], MT_STRIDE,
+        a = _lib.sd_mt_generate_args(self.state.data_ptr(), table.data_ptr(), table.shape[0], stride,
                                      self.words.data_ptr(), n, self.ws.data_ptr(), self.ws.numel())
         _lib.check(lib.sd_mt19937_generate(C.byref(a), C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)),
                    "sd_mt19937_generate")

@@ -93,7 +93,7 @@ NGRAM_CASES = [
     ("ng_greedy_g4_n3_eos", 4096, "bf16", ("multi", 3), 4, ("greedy", 1.0, 0, 1.0), 3, False, 60, "likely", [0, 1]),
     ("ng_multi_g4_n3_fp32", 4096, "fp32", ("multi", 3), 4, ("multinomial", 1.0, 0, 1.0), 3, False, 40, [1], [0]),
     ("ng_llama_nucleus_g8", 128256, "bf16", ("multi", 3), 8, ("nucleus", 1.0, 0, 0.9), 3, False, 24,
-     [128001, 128009], [0]),
+     [128001, 128009], [0, 1, 2]),
 ]
 
 DT = {"bf16": torch.bfloat16, "fp32": torch.float32}

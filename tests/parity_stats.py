@@ -13,10 +13,12 @@ def summary_lines():
     if not (DIVERGENCES or TIE_DIVERGENCES or NUCLEUS_ROWS or DRAW_CLOSE_CALLS):
         return []
     inexact = {k.split("=", 1)[1]: v for k, v in NUCLEUS_ROWS.items() if k.startswith("inexact=")}
+    variants = {k.split("=", 1)[1]: v for k, v in sorted(NUCLEUS_ROWS.items()) if k.startswith("variant=")}
     return [
         f"torch-CPU rounding divergences: {len(DIVERGENCES)} (each equal to the exact oracle) {DIVERGENCES[:8]}",
         f"nucleus tie-order divergences: {len(TIE_DIVERGENCES)}",
         f"nucleus rows checked: {NUCLEUS_ROWS['checked']}, flagged INEXACT: {NUCLEUS_ROWS['inexact']}, "
         f"INEXACT rows by matching oracle: {inexact}",
+        f"nucleus rows per processor variant: {variants}",
         f"perf-mode close calls (|u - p/q| within fp32 rounding): {len(DRAW_CLOSE_CALLS)} {DRAW_CLOSE_CALLS[:4]}",
     ]

@@ -99,6 +99,11 @@ SPEC_GRID = [
     (1, 4, 128256, torch.bfloat16, "topk50_t08", 18),
     (1, 8, 128256, torch.bfloat16, "nucleus09", 19),
     (1, 4, 4096, torch.float16, "multi_t1", 20),
+    # nucleus at the production shape (Llama-3 vocab, bf16): >= 16 rows through check_spec
+    (4, 4, 128256, torch.bfloat16, "nucleus09", 21),
+    (4, 4, 128256, torch.bfloat16, "nucleus05_t07", 22),
+    (4, 4, 128256, torch.bfloat16, "topknucleus", 23),
+    (4, 8, 128256, torch.bfloat16, "nucleus09", 24),
 ]
 
 
@@ -178,6 +183,8 @@ def check_spec(sd, tl, dl, ids, proc, seed, stops=(), skip=False):
         note_divergence(match[0], f"spec seed={seed} row={b}")
         if proc.kind in ("nucleus", "topknucleus"):
             NUCLEUS_ROWS["checked"] += 1
+            NUCLEUS_ROWS[f"variant={proc.kind}(T={proc.temperature:g},k={proc.top_k},p={proc.top_p:g})"
+                         f"@V{tl.shape[-1]}"] += 1
             if st[b] & sd.lib.SD_ROW_NUCLEUS_INEXACT:   # held to the same integer match, and counted
                 NUCLEUS_ROWS["inexact"] += 1
                 NUCLEUS_ROWS["inexact=" + match[0]] += 1
