@@ -136,7 +136,7 @@ class EngineStep:
         self.B, self.g, self.V = B, g, V
         self.noise, self.row0 = noise, row0
         self.draft = torch.empty(B, g, dtype=torch.long, device=dev)
-        self.stash = type(noise).__name__ == "PhiloxNoise"
+        self.stash = True   # the draws return their rows' (max, Σexp) in both noise modes
         self.dstats = torch.empty(g, B, 2, dtype=torch.float32, device=dev)   # drafter rows' (max, Σexp)
         self.stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
         self.trows = [tl[:, t, :] for t in range(g)]

@@ -49,12 +49,30 @@ __device__ __forceinline__ uint32_t mag(uint32_t a, uint32_t b) {
     return (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
 }
 
+// (s & k) ^ y in one v_bitop3_b32 (truth table 0x6c over (s, y, k)); k lives in an SGPR
+__device__ __forceinline__ uint32_t and_xor(uint32_t s, uint32_t y, uint32_t k) {
+    return __builtin_amdgcn_bitop3_b32(s, y, k, 0x6c);
+}
+
 __device__ __forceinline__ uint32_t temper(uint32_t y) {
     y ^= (y >> 11);
-    y ^= (y << 7) & 0x9d2c5680u;
-    y ^= (y << 15) & 0xefc60000u;
+    y = and_xor(y << 7, y, 0x9d2c5680u);
+    y = and_xor(y << 15, y, 0xefc60000u);
     y ^= (y >> 18);
     return y;
+}
+
+// x[q-681] ^ mag(a0, b0) ^ mag(a1, b1) ^ mag(a2, b2) with the three mags folded together: the
+// shifted halves XOR linearly, (upper(A) | lower(B)) >> 1 with A, B the XORs of the a's and b's,
+// and the matrix term is taken once on the parity of the b's low bits (bit 0 of that same word).
+// Seven VALU operations for the round's word instead of ~20.
+__device__ __forceinline__ uint32_t mag3(uint32_t c, uint32_t a0, uint32_t b0, uint32_t a1, uint32_t b1,
+                                         uint32_t a2, uint32_t b2) {
+    const uint32_t A = __builtin_amdgcn_bitop3_b32(a0, a1, a2, 0x96);           // a0 ^ a1 ^ a2
+    const uint32_t B = __builtin_amdgcn_bitop3_b32(b0, b1, b2, 0x96);
+    const uint32_t Y = __builtin_amdgcn_bitop3_b32(A, B, 0x80000000u, 0xe4);   // upper(A) | lower(B)
+    const uint32_t m = (uint32_t)((int32_t)(Y << 31) >> 31);                    // -(Y & 1)
+    return and_xor(m, (Y >> 1) ^ c, 0x9908b0dfu);
 }
 
 __device__ __forceinline__ uint32_t untemper(uint32_t y) {
@@ -81,16 +99,17 @@ constexpr int kBlk = kN - 1;           // 623 positions per round
 constexpr int kMtThreads = 640;        // 10 waves: a round's 623 positions, one per thread
 constexpr int kBack = 1078;            // the oldest input of a round, q - 1078
 
-__device__ __forceinline__ void ring_put(uint32_t* r, int64_t q, uint32_t x) {
-    const int i = (int)(q & (kRing - 1));
+__device__ __forceinline__ void ring_put(uint32_t* r, int q, uint32_t x) {
+    const int i = q & (kRing - 1);
     r[i] = x;
     r[i + kRing] = x;
 }
 
 // Extend the ring holding x[0 .. 624) to x[len), calling out(q, x) for q in [624, len).  Whole
-// workgroup of kMtThreads; the caller put x[0 .. 624) in the ring and synchronised.
+// workgroup of kMtThreads; the caller put x[0 .. 624) in the ring and synchronised.  Positions are
+// 32-bit (a substream is at most a few million words): the round's index math stays in one VGPR.
 template <typename Out>
-__device__ __forceinline__ void mt_extend(uint32_t* r, int64_t len, Out out) {
+__device__ __forceinline__ void mt_extend(uint32_t* r, int len, Out out) {
     const int t = threadIdx.x;
     // [624, 1078): the plain recurrence, one round of two chained positions per thread
     if (t < kLag) {
@@ -103,11 +122,11 @@ __device__ __forceinline__ void mt_extend(uint32_t* r, int64_t len, Out out) {
         out(q2, x2);
     }
     lds_barrier();
-    for (int64_t q0 = kBack; q0 < len; q0 += kBlk) {
-        if (t < kBlk) {
-            const int64_t q = q0 + t;
-            const uint32_t* b = r + (int)(q & (kRing - 1)) + kRing - kBack;   // b[k] = x[q - 1078 + k]
-            const uint32_t x = b[397] ^ mag(b[0], b[1]) ^ mag(b[227], b[228]) ^ mag(b[454], b[455]);
+    const bool act = t < kBlk;
+    for (int q0 = kBack, q = kBack + t; q0 < len; q0 += kBlk, q += kBlk) {
+        if (act) {
+            const uint32_t* b = r + (q & (kRing - 1)) + kRing - kBack;   // b[k] = x[q - 1078 + k]
+            const uint32_t x = mag3(b[397], b[0], b[1], b[227], b[228], b[454], b[455]);
             ring_put(r, q, x);
             out(q, x);
         }
@@ -125,7 +144,7 @@ __global__ void __launch_bounds__(kMtThreads) k_mt_base(const sd_mt_state* __res
         base[t] = w;
     }
     __syncthreads();
-    mt_extend(ring, kBaseLen, [&](int64_t q, uint32_t x) {
+    mt_extend(ring, kBaseLen, [&](int q, uint32_t x) {
         if (q < kBaseLen) base[q] = x;
     });
 }
@@ -177,7 +196,7 @@ __global__ void __launch_bounds__(64) k_mt_jump(const sd_mt_state* __restrict__ 
 
 // ----------------------------------------------------------------------------------------- gen
 __global__ void __launch_bounds__(kMtThreads) k_mt_gen(const sd_mt_state* __restrict__ st, const uint32_t* __restrict__ base,
-                                                       const uint32_t* __restrict__ partial, int nch, uint32_t* __restrict__ out,
+                                                       const uint32_t* __restrict__ partial, int /*nch: SD_MT_JUMP_CHUNKS*/, uint32_t* __restrict__ out,
                                                        int64_t n, int64_t stride) {
     __shared__ uint32_t ring[2 * kRing];
     const int s = blockIdx.x, t = threadIdx.x;
@@ -189,16 +208,22 @@ __global__ void __launch_bounds__(kMtThreads) k_mt_gen(const sd_mt_state* __rest
         if (s == 0) {
             w = base[st->tau0 + t];
         } else {
+            // every chunk partial in flight at once (a load -> xor loop waited for each in turn:
+            // 16 dependent round trips before the first round)
             w = 0u;
-            const uint32_t* p = partial + (size_t)(s - 1) * nch * kN + t;
-            for (int c = 0; c < nch; ++c) w ^= p[(size_t)c * kN];
+            const uint32_t* p = partial + (size_t)(s - 1) * SD_MT_JUMP_CHUNKS * kN + t;
+            uint32_t pv[SD_MT_JUMP_CHUNKS];
+#pragma unroll
+            for (int c = 0; c < SD_MT_JUMP_CHUNKS; ++c) pv[c] = p[(size_t)c * kN];
+#pragma unroll
+            for (int c = 0; c < SD_MT_JUMP_CHUNKS; ++c) w ^= pv[c];
         }
         ring_put(ring, t, w);
         if (t < len) o[t] = temper(w);
     }
     __syncthreads();
-    mt_extend(ring, len, [&](int64_t q, uint32_t x) {
-        if (q < len) o[q] = temper(x);
+    mt_extend(ring, (int)len, [&](int q, uint32_t x) {
+        if (q < (int)len) o[(uint32_t)q] = temper(x);
     });
 }
 

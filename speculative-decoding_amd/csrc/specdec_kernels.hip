@@ -2786,6 +2786,7 @@ int spin_limit() {
 
 #include "sd_threshold.inc"
 #include "sd_draw_nucleus.inc"
+#include "sd_draw_stream.inc"
 
 namespace {
 
@@ -3077,6 +3078,56 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
     return SD_OK;
 }
 
+// STREAM multinomial rows (T = 1, no processor, 16-bit, aligned) in one pass (k_draw_stream,
+// sd_draw_stream.inc): 1 if launched, 0 if the shape needs the three-launch path (row statistics,
+// k_rowsample, k_sample_finalize), < 0 on a launch error.  Poll mode only: the grid's consumers
+// must leave room for every producer (the occupancy check), and sd_set_poll_policy must allow it;
+// SD_DRAW_STREAM=0 turns it off (A/B, tests).
+int32_t launch_draw_stream(const sd::Plan& P, void* stream) {
+    if (P.noise.mode != SD_NOISE_STREAM || !P.t_stoch || P.tT != 1.0f || P.t_keep || P.tdt == SD_F32) return 0;
+    if (P.token_prob || P.keep_out || P.B > kCntMax || !poll_allowed()) return 0;
+    if (const char* e = getenv("SD_DRAW_STREAM"))
+        if (!atoi(e)) return 0;
+    const bool al = (reinterpret_cast<uintptr_t>(P.trow[0]) & 15) == 0 && (P.tstride * 2) % 16 == 0;
+    const int n_span = (int)((P.V + kThreads * 8 - 1) / (kThreads * 8));
+    if (!al || P.V < 8 || n_span > 128) return 0;
+    if ((int64_t)n_span * sd::kDsRecs * 16 > (int64_t)(max_chunks(P.V) + 1) * (int64_t)sizeof(sd::ResPart)) return 0;
+    static int cap[2][64];
+    const int di = P.tdt == SD_BF16 ? 0 : 1;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (cap[di][dev] == 0) {
+        int per_cu = 0, cus = 0;
+        const void* kern = P.tdt == SD_BF16 ? (const void*)sd::k_draw_stream<SD_BF16> : (const void*)sd::k_draw_stream<SD_F16>;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = cus = 0;
+        cap[di][dev] = per_cu * cus > 0 ? per_cu * cus : -1;
+    }
+    if (cap[di][dev] <= 0 || 2 * P.B > cap[di][dev]) return 0;
+    sd::DrawStream A{};
+    A.rows = static_cast<const char*>(P.trow[0]);
+    A.stride_bytes = P.tstride * 2;
+    A.recs = reinterpret_cast<uint4*>(P.rpart);
+    A.cnt = P.cnt;
+    A.next_token = P.next_token;
+    A.nt_stride = P.next_token_stride;
+    A.row_stats = P.row_stats;
+    A.row_status = P.row_status;
+    A.words_used = P.words_used;
+    A.status_or = P.status_or;
+    A.ts = P.ts;
+    A.noise = P.noise;
+    A.V = P.V;
+    A.n_span = n_span;
+    A.spin_limit = P.spin_limit;
+    A.rows_total = P.B;
+    const dim3 grid(n_span, P.B);
+    if (P.tdt == SD_BF16) SD_LAUNCH((sd::k_draw_stream<SD_BF16>), grid, dim3(kThreads), stream, A);
+    else SD_LAUNCH((sd::k_draw_stream<SD_F16>), grid, dim3(kThreads), stream, A);
+    return 1;
+}
+
 // greedy sd_sample rows in one pass (k_draw_lean<GREEDY>): 1 if launched, 0 if the shape needs the
 // three-launch path (statistics, per-chunk argmax, finalize), < 0 on a launch error
 int32_t launch_greedy_lean(const sd::Plan& P, void* stream) {
@@ -3363,6 +3414,7 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
         if (P.B > kCntMax || max_chunks(P.V) > kTailChunks) return SD_ERR_UNSUPPORTED;
         return launch_draw(P, stream);   // one pass; the row's last arrival writes the outputs
     }
+    if (const int32_t st = launch_draw_stream(P, stream)) return st < 0 ? st : SD_OK;   // STREAM, one pass
     if (!P.t_stoch && P.B <= kCntMax) {   // greedy (either noise mode: no noise is drawn)
         const int32_t st = launch_greedy_lean(P, stream);
         if (st < 0) return st;

@@ -234,15 +234,16 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
                     first_token_callback(idx)
         return outs
 
-    # perf mode: each draw also returns its row's (max, Σexp), so verify reads only target rows
-    stash = isinstance(noise, PhiloxNoise)
+    # each draw also returns its row's (max, Σexp) — free in the one-pass draws of both noise modes
+    # (k_draw_lean, k_draw_stream) — so the verify's statistics pass reads only target rows
+    stash = True
     dstats = torch.empty(max(gamma, 1), B, 2, dtype=torch.float32, device=dev) if stash else None
     past = ctx.drafter(input_ids, attention_mask=attention_mask, use_cache=True).past_key_values   # :206
     # Philox: the all-finished test of :212 is read one window late (pinned copy behind an event), so
     # the host queues the next window while the GPU runs this one.  A window over all-finished rows
     # changes nothing, so the outputs are the reference's.  STREAM keeps the exact check: such a
     # window would still consume generator words.
-    probe = _FinishedProbe(finished, err) if stash else None
+    probe = _FinishedProbe(finished, err) if isinstance(noise, PhiloxNoise) else None
     step = 0
     while step < gen_len:                                                 # :211
         if probe is not None:

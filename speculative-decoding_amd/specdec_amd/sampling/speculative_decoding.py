@@ -20,7 +20,7 @@ import torch
 from torch.nn import Module
 
 from .. import _lib
-from ..noise import PhiloxNoise, StreamNoise, default_noise, noise_session
+from ..noise import StreamNoise, default_noise, noise_session
 from ..ops import proc_spec, sample_rows, verify
 from ..utils.caching import prune_cache
 from ..utils.logits_processor import GreedyProcessor, LogitsProcessor
@@ -137,11 +137,11 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         if t in stops:
             return input_ids[0, prompt_len:cur].tolist(), 0
 
-    # perf mode: each draw also returns its row's (max, Σexp), so verify reads only target rows.
-    # Not for top-k / nucleus processors: their stats would need the draw's threshold search,
+    # each draw also returns its row's (max, Σexp) (both noise modes), so verify reads only target
+    # rows.  Not for top-k / nucleus processors: their stats would need the draw's threshold search,
     # which the nucleus draw skips (k_draw_nuc, rejection against the nucleus); the verify
     # thresholds all its rows in one launch anyway.
-    stash = isinstance(noise, PhiloxNoise) and torch.device(drafter.device) == torch.device(dev) and not spec.keeps
+    stash = torch.device(drafter.device) == torch.device(dev) and not spec.keeps
     dstats = torch.empty(max(gamma, 1), 1, 2, dtype=torch.float32, device=dev) if stash else None
     while cur < total_len:                                       # :105
         g = min(gamma, total_len - cur - 1)                      # :106
