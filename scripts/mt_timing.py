@@ -1,7 +1,8 @@
 """Device STREAM generator timing (GPU box): sd_mt19937_generate for one engine drafter draw's
-words (2 * 32 * 128256) at several substream strides, HIP events on the launch stream.
+words at several substream strides, HIP events on the launch stream.  Default n_words: one
+bench-shape STREAM engine step's pool (4 drafter draws + verify at B = 32, V = 128256).
 
-    python scripts/mt_timing.py [n_words]
+    STRIDES=131072,196608 python scripts/mt_timing.py [n_words]
 """
 import json
 import os
@@ -15,9 +16,10 @@ import torch  # noqa: E402
 
 from specdec_amd import noise as nz  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 2 * 32 * 128256
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 41042048
+strides = [int(x) for x in os.environ.get("STRIDES", "131072,196608,262144,327680,393216").split(",")]
 g = torch.Generator().manual_seed(1)
-for stride in (16384, 32768, 65536, 131072):
+for stride in strides:
     nz.MT_STRIDE, nz._STRIDE_ENV = stride, str(stride)
     d = nz._DeviceMT("cuda", g.get_state())
     t0 = time.perf_counter()

@@ -1,7 +1,8 @@
 """Per-workgroup phase timing of one perf-mode verify step (diagnostic; GPU box).
 
 Loads the SD_PHASE_TIMING build (make -C speculative-decoding_amd timing), runs the bench
-shape (engine rule, B=32, γ=4, V=128256 bf16, Philox) and prints, per kernel, when workgroups
+shape (engine rule, B=32, γ=4, V=128256 bf16, Philox; B=1 RULE=spec: configs[1]'s multinomial
+verify over γ+1 target rows) and prints, per kernel, when workgroups
 start / reach each phase relative to the kernel's first start (µs, s_memrealtime = 100 MHz).
 """
 import os
@@ -17,11 +18,14 @@ import torch  # noqa: E402
 from specdec_amd import _lib, ops  # noqa: E402
 from specdec_amd.noise import PhiloxNoise  # noqa: E402
 
-B, G, V = 32, 4, 128256
+B, G, V = int(os.environ.get("B", 32)), 4, 128256
+SPEC = os.environ.get("RULE", "engine") == "spec"
+NT = G + 1 if SPEC else G
+LEAN = os.environ.get("SD_LEAN_VERIFY", "1") != "0" and B <= 8
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
-tl = (torch.randn(B, G, V, device=dev, generator=g) * 3).to(torch.bfloat16)
-dl = (tl.float() + torch.randn(B, G, V, device=dev, generator=g)).to(torch.bfloat16)
+tl = (torch.randn(B, NT, V, device=dev, generator=g) * 3).to(torch.bfloat16)
+dl = (tl[:, :G].float() + torch.randn(B, G, V, device=dev, generator=g)).to(torch.bfloat16)
 ids = dl.float().argmax(-1)
 noise = PhiloxNoise(seed=1)
 # the bench's verify: drafter rows' (max, Σexp) come from the draws, k_stats reads target rows only
@@ -32,7 +36,8 @@ ts = torch.zeros(16384 * 16, dtype=torch.int64, device=dev)
 
 
 def step():
-    return ops.verify([tl[:, t] for t in range(G)], [dl[:, t] for t in range(G)], ids, _lib.SD_RULE_ENGINE,
+    return ops.verify([tl[:, t] for t in range(NT)], [dl[:, t] for t in range(G)], ids,
+                      _lib.SD_RULE_SPEC if SPEC else _lib.SD_RULE_ENGINE,
                       ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise, torch.tensor([], dtype=torch.long, device=dev),
                       draft_row_stats=dstats)
 
@@ -53,7 +58,10 @@ for rep in range(3):
     torch.cuda.synchronize()
     t = ts.view(-1, 16).cpu().numpy().astype(np.int64)
     print(f"--- rep {rep}")
-    for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "loop_end", "arrived", "decided", "dec_stats", "dec_ratios"]),
+    for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "merged", "arrived", "decided", "dec_stats", "dec_ratios",
+                                                        "stream_done", "pf_late", "rec_stored"]
+                   if not LEAN else ["start", "merged", "rec_stored", "decided", "dec_stats", "dec_ratios",
+                                     "loads_landed", "rows_reduced", "pf_late", "poll_1st", "-", "poll_done"]),
                                  ("k_sample_finish", 16384 - 64, 16384, ["start", "prologue", "body_end", "arrived",
                                                             "tail_S", "cdf_pick", "finalized", "cdf_select",
                                                             "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"]),

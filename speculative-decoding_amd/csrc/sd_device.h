@@ -222,6 +222,28 @@ __device__ __forceinline__ uint4 ld_coh16(const void* p) {
     return make_uint4(w.x, w.y, w.z, w.w);
 }
 
+// five coherent 16-byte loads in flight together, one wait (pollers that read several records:
+// separate ld_coh16 calls cost one round trip each).  Unused slots take any valid address.
+__device__ __forceinline__ void ld_coh16x5(const void* p0, const void* p1, const void* p2, const void* p3,
+                                           const void* p4, uint4* out) {
+    sd_u32x4 a, b, c, d, e;
+    asm volatile(
+        "global_load_dwordx4 %0, %5, off sc1\n\t"
+        "global_load_dwordx4 %1, %6, off sc1\n\t"
+        "global_load_dwordx4 %2, %7, off sc1\n\t"
+        "global_load_dwordx4 %3, %8, off sc1\n\t"
+        "global_load_dwordx4 %4, %9, off sc1\n\t"
+        "s_waitcnt vmcnt(0)"
+        : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d), "=&v"(e)
+        : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4)
+        : "memory");
+    out[0] = make_uint4(a.x, a.y, a.z, a.w);
+    out[1] = make_uint4(b.x, b.y, b.z, b.w);
+    out[2] = make_uint4(c.x, c.y, c.z, c.w);
+    out[3] = make_uint4(d.x, d.y, d.z, d.w);
+    out[4] = make_uint4(e.x, e.y, e.z, e.w);
+}
+
 // this wave's coherent stores have completed (s_waitcnt 0), and the compiler keeps order
 __device__ __forceinline__ void coh_wait() {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);

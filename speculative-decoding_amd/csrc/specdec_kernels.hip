@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <climits>
+#include <cstdio>
 #include <cmath>
 #include <cstdlib>
 #include <map>
@@ -104,6 +105,7 @@ struct Plan {
     float* rq;
     Decision* dec;
     ResPart* rpart;
+    uint4* srec;          // k_stats' poll-mode records: rpart, or past the sampler's records (k_verify_lean)
     int32_t* keep_hist;   // threshold scratch
     uint32_t* thr_part;   // 16-bit thresholds (sd_threshold.inc): per (row, slice) max key | NaN-inf flag
     float* thr_tail;      //   per (row, slice) Σexp below the window / tie counts
@@ -282,7 +284,7 @@ __device__ __forceinline__ const void* slot_row(const Plan& P, int b, int s) {
     return static_cast<const char*>(P.drow[s - P.n_tslots]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
 }
 
-__device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd);
+__device__ __forceinline__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd);
 __device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64_t woff, bool* overrun);
 
 // What the perf-mode decision needs of draft i, gathered by one thread while the row statistics
@@ -320,7 +322,7 @@ __device__ __forceinline__ void pf_late(const Plan& P, int b, int i, DraftPf& pf
     bool ovr = false;
     pf.u = draw_uniform(P, b, i, 0, &ovr);   // perf mode: Philox, no stream words
 }
-__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out = nullptr,
+__device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out = nullptr,
                            bool publish = true, bool coh = true, const uint32_t* poll_epoch = nullptr);
 
 // Poll-mode tag of k_stats' partial record (slot s, chunk c) of sequence b (k_draw_lean's protocol,
@@ -331,7 +333,7 @@ __device__ __forceinline__ uint32_t stats_tag(uint32_t epoch, int b, int s, int 
     return h | 1u;
 }
 __device__ __forceinline__ uint4* stats_rec(const Plan& P, int b, int s, int c) {
-    return reinterpret_cast<uint4*>(P.rpart) + ((int64_t)b * P.stat_slots + s) * P.n_chunks + c;
+    return P.srec + ((int64_t)b * P.stat_slots + s) * P.n_chunks + c;
 }
 
 // Arrival at a per-sequence counter (thread 0, after storing its partials with st_coh): true for
@@ -378,29 +380,47 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
     const int wg_id = blockIdx.y * gridDim.x + blockIdx.x;
     SD_TS(wg_id, 0);
+    // The kernel-argument fields the first row loads depend on, read in one straight-line block (no
+    // branch between them, both row tables indexed unconditionally): the scalar loads then go out
+    // together with one wait, instead of a chain of ~10 dependent waits that put the first row
+    // load ~3 us after the start at batch 1.
+    const int gx = (int)gridDim.x;
+    const int xa = P.xcd_affine, nt = P.n_tslots;
+    const int64_t tstr = P.tstride, dstr = P.dstride;
     int b, s, chunk;
-    if (P.xcd_affine) {
-        int item;
-        affine_split(wg_id, slot_cnt * (int)gridDim.x, b, item);
-        s = slot_lo + item / (int)gridDim.x;
-        chunk = item % (int)gridDim.x;
-    } else {
-        b = blockIdx.y / slot_cnt;
-        s = slot_lo + blockIdx.y % slot_cnt;
-        chunk = blockIdx.x;
+    {
+        int ba, item;
+        affine_split(wg_id, slot_cnt * gx, ba, item);
+        const int bn = (int)blockIdx.y / slot_cnt, sn = slot_lo + (int)blockIdx.y % slot_cnt;
+        b = xa ? ba : bn;
+        s = xa ? slot_lo + item / gx : sn;
+        chunk = xa ? item % gx : (int)blockIdx.x;
     }
+    const bool is_t = s < nt;
+    const char* tp = static_cast<const char*>(P.trow[is_t ? s : 0]);
+    const char* dp = static_cast<const char*>(P.drow[is_t ? 0 : s - nt]);
     const int r = b * P.slots + s;
-    const void* row = slot_row(P, b, s);
-    // poll mode: this call's epoch of sequence b (thread 0, beside the first loads)
+    const void* row = is_t ? tp + b * tstr * (P.tdt == SD_F32 ? 4 : 2) : dp + b * dstr * (P.ddt == SD_F32 ? 4 : 2);
+    // poll mode: this call's epoch of sequence b (thread 0), issued AFTER the first row loads and
+    // kept in a register until the record: loads complete in order, so an atomic issued first
+    // held back the wave's first stage (batch 1: stream done 3.2 vs ~1.4 us after the start)
     __shared__ uint32_t s_epoch;
-    if (TAIL && P.kpoll && threadIdx.x == 0)
-        s_epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const bool ep_thread = TAIL && P.kpoll && threadIdx.x == 0;
+    uint32_t ep_reg = 0u;
+    bool ep_read = false;
+    auto read_epoch = [&]() {
+        if (ep_thread && !ep_read) ep_reg = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ep_read = true;
+    };
     // TAIL: drafted ids now (consumed after the loop), their logits right after it, so a
-    // workgroup that turns out to be its sequence's last arrival has them in registers
+    // workgroup that turns out to be its sequence's last arrival has them in registers.  Poll mode
+    // knows its consumer up front (the last span of the last slot): the producers skip the
+    // prefetch, whose dependent loads the workgroup barrier below would wait for before their
+    // records go out (batch 1: records at 5.8 instead of ~2 us after the launch)
     DraftPf pf;
-    const int pf_i = TAIL ? pf_draft(P) : -1;
+    const bool pf_here = TAIL && (!P.kpoll || (s == P.stat_slots - 1 && chunk == P.n_chunks - 1));
+    const int pf_i = pf_here ? pf_draft(P) : -1;
     if (TAIL) pf_early(P, b, pf_i, pf);
-    const bool is_t = s < P.n_tslots;
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
     const RowKeep kp = has_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
@@ -473,6 +493,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
         uint4 buf[kPipe];
 #pragma unroll
         for (int d = 0; d < kPipe; ++d) buf[d] = vb[stage_of(d < nfull ? d : nfull - 1) * kThreads];
+        read_epoch();
         int it = 0;
         for (; it + kPipe <= nfull; it += kPipe) {
 #pragma unroll
@@ -502,7 +523,11 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
         for (int k = 0; k < VEC; ++k) x[k] = (e0 + k < hi) ? load_one<DT>(row, e0 + k) : 0.f;
         consume(x, e0, std::true_type{});
     }
+    read_epoch();
+    if (ep_thread) s_epoch = ep_reg;
+    SD_TS(wg_id, 6);
     if (TAIL) pf_late(P, b, pf_i, pf);
+    SD_TS(wg_id, 7);
     // workgroup combine (fixed order): DPP wave merge, then the 4 waves through LDS
     merge_step<kDppQuad1032>(m, acc);
     merge_step<kDppQuad2301>(m, acc);
@@ -529,6 +554,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
         else
             st_coh(P.part + (int64_t)r * P.n_chunks + chunk, make_float2(M, S));
     }
+    SD_TS(wg_id, 8);
     if constexpr (TAIL) {
         __shared__ int s_last;
         if (poll) {
@@ -581,7 +607,7 @@ __device__ __forceinline__ float prob_dyn(int dt, const void* row, int64_t j, fl
 // Row statistics of every slot of sequence b, combined from the k_stats partials into LDS
 // (all waves of the block).  Stats stay in LDS for the block's own use: re-reading them from
 // global memory after a barrier could hit a line another block on this CU cached earlier.
-__device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
+__device__ __forceinline__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
     // drafter rows whose stats came with their draws (sd_sample row_stats): no partials
     for (int s = P.stat_slots + (int)threadIdx.x; s < P.slots; s += (int)blockDim.x) {
@@ -622,7 +648,7 @@ __device__ void seq_stats(const Plan& P, int b, float2* lstat, bool publish) {
 }
 
 // Raw target / drafter values at drafted id tok of draft i (0 for an out-of-range id).
-__device__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd) {
+__device__ __forceinline__ void fetch_drafted(const Plan& P, int b, int i, int64_t tok, float* xt, float* xd) {
     *xt = 0.f;
     *xd = 0.f;
     if (tok >= 0 && tok < P.V) {
@@ -752,7 +778,7 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
     return d;
 }
 
-__device__ void publish_decision(const Plan& P, int b, const Decision& d) {
+__device__ __forceinline__ void publish_decision(const Plan& P, int b, const Decision& d) {
     const int g = P.gamma;
     const bool pruned = P.rule == SD_RULE_SPEC && d.n < g && d.stop_index < 0;   // the engine never prunes
     if (P.prune_drafter) P.prune_drafter[b] = pruned ? g - d.n : 0;
@@ -918,7 +944,7 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
 // uniforms, the walk.  Every per-draft input was prefetched during the stream (DraftPf), so the
 // tail has one memory round trip (the partials).  With the drafter stats prefetched (P.dstats)
 // the wave that reduces target slot i tests draft i at once: one barrier before the walk.
-__device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out, bool publish, bool coh,
+__device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out, bool publish, bool coh,
                            const uint32_t* poll_epoch) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
     __shared__ float lp[SD_MAX_GAMMA], lq[SD_MAX_GAMMA];
@@ -934,23 +960,36 @@ __device__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, D
         constexpr int kMaxSlotsPerWave = (SD_MAX_GAMMA + 1 + 3) / 4;
         float2 v[kMaxSlotsPerWave];
         if (poll_epoch) {   // poll mode: each record re-read until it carries this call's tag (bounded)
+            static_assert(kMaxSlotsPerWave <= 5, "ld_coh16x5");
             const uint32_t ep = *poll_epoch;
+            // the wave's records all in flight at once (one round trip), then the stragglers
+            const uint4* rp[5];
+            bool need[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) {
+                const int s = w + k * nw;
+                need[k] = k < kMaxSlotsPerWave && s < P.n_tslots && lane < P.n_chunks;
+                rp[k] = need[k] ? stats_rec(P, b, s, lane) : stats_rec(P, b, 0, 0);
+            }
+            uint4 r[5];
+            ld_coh16x5(rp[0], rp[1], rp[2], rp[3], rp[4], r);
+            SD_TS(wg_id, 9);
 #pragma unroll
             for (int k = 0; k < kMaxSlotsPerWave; ++k) {
                 const int s = w + k * nw;
                 v[k] = make_float2(-INFINITY, 0.f);
-                if (s < P.n_tslots && lane < P.n_chunks) {
-                    const uint4* rp = stats_rec(P, b, s, lane);
+                if (need[k]) {
                     const uint32_t tag = stats_tag(ep, b, s, lane);
-                    uint4 r = ld_coh16(rp);
-                    for (int spin = 0; r.z != tag && spin_more(spin, P.spin_limit); ++spin) {
+                    uint4 rr = r[k];
+                    for (int spin = 0; rr.z != tag && spin_more(spin, P.spin_limit); ++spin) {
                         __builtin_amdgcn_s_sleep(1);
-                        r = ld_coh16(rp);
+                        rr = ld_coh16(rp[k]);
                     }
-                    v[k] = r.z == tag ? make_float2(__uint_as_float(r.x), __uint_as_float(r.y))
-                                      : make_float2(0.f, NAN);   // timeout: the row is flagged invalid
+                    v[k] = rr.z == tag ? make_float2(__uint_as_float(rr.x), __uint_as_float(rr.y))
+                                       : make_float2(0.f, NAN);   // timeout: the row is flagged invalid
                 }
             }
+            SD_TS(wg_id, 11);
         } else {
 #pragma unroll
             for (int k = 0; k < kMaxSlotsPerWave; ++k) {
@@ -1134,7 +1173,7 @@ __device__ __forceinline__ void stream_race(const sd_noise& nz, int64_t woff, co
 constexpr float kCandTol = 1.0f - 64.0f * 5.9604645e-08f;
 
 template <int TDT, int DDT, int NZ, int EPT, bool FAST>
-__device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float2 mst, float2 msd_in) {
+__device__ __forceinline__ void resid_body(const Plan& P, const Decision& d, int b, int c, float2 mst, float2 msd_in) {
     __shared__ float ldsf[8];
     __shared__ int32_t lcount;
     __shared__ float lres[kMaxCand], le[kMaxCand];
@@ -1254,7 +1293,7 @@ __device__ void resid_body(const Plan& P, const Decision& d, int b, int c, float
 }
 
 template <int TDT, int NZ, int EPT, bool FAST>
-__device__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2 mst) {
+__device__ __forceinline__ void prow_body(const Plan& P, const Decision& d, int b, int c, float2 mst) {
     __shared__ float ldsf[8];
     __shared__ int32_t ldsi[8];
     constexpr int VEC = Elem<TDT>::kVec, NV = EPT / VEC;
@@ -1354,7 +1393,7 @@ __device__ __forceinline__ float resid_mass(const Plan& P, int b, float* wmax) {
 // The token of sequence b from the argmax-candidate partials (one wave): residual candidates
 // evaluated exactly as fl(fl(res / S) / E), the engine's multinomial(p) fallback, bonus / p-row
 // argmax.  x = -1 when nothing is sampled.
-__device__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, float& mass, int32_t& status) {
+__device__ __forceinline__ void pick_wave(const Plan& P, int b, const Decision& d, int64_t& x, float& mass, int32_t& status) {
     const int lane = threadIdx.x & 63;
     const ResPart* rp = P.rpart + (int64_t)b * P.rn_chunks;
     if (d.mode == kModeResid) {
@@ -2787,6 +2826,7 @@ int spin_limit() {
 #include "sd_threshold.inc"
 #include "sd_draw_nucleus.inc"
 #include "sd_draw_stream.inc"
+#include "sd_verify_lean.inc"
 
 namespace {
 
@@ -2822,6 +2862,7 @@ void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     P.dec = c.take<Decision>(B);
     // + 1 per row: room for 16-byte records padded to whole 128-B lines per row (k_draw_lean)
     P.rpart = c.take<ResPart>((size_t)(B > rows_total ? B : rows_total) * (nc + 1));
+    P.srec = reinterpret_cast<uint4*>(P.rpart);
     P.keep_hist = c.take<int32_t>((size_t)rows_total * kThreshScratchInts);
     P.thr_part = c.take<uint32_t>((size_t)rows_total * kThrMaxSlices);
     P.thr_tail = c.take<float>((size_t)rows_total * kThrMaxSlices);
@@ -3076,6 +3117,77 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
     A.affine = affine_env && P.B % 8 == 0;
     SD_LAUNCH((k_draw_lean<DT, NST, GREEDY>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
     return SD_OK;
+}
+
+// The one-launch verify of a few sequences (sd_verify_lean.inc): 1 launched, 0 not applicable (the
+// caller runs k_stats + k_sample), < 0 a launch error.  Perf mode with the drafter stats from the
+// draws, no top-k / nucleus, 16-bit rows of one dtype, V <= 64 spans, every row 16-byte aligned, and
+// the whole grid resident (every workgroup polls).  Up to kLeanVerifyMaxB sequences by default;
+// SD_LEAN_VERIFY=0 turns it off, =1 allows any batch the occupancy check admits (A/B, tests).
+constexpr int kLeanVerifyMaxB = 8;
+
+static void lean_why(int k) {
+    static const bool dbg = getenv("SD_LEAN_DEBUG") != nullptr;
+    if (dbg) fprintf(stderr, k ? "launch_verify_lean: not applicable (%d)\n" : "launch_verify_lean: launched\n", k);
+}
+
+int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
+    if (P0.noise.mode == SD_NOISE_STREAM || !P0.tails || P0.dec_in_sample) { lean_why(1); return 0; }
+    if (P0.t_keep || P0.d_keep || !P0.dstats || P0.draft_is_probs || P0.stat_slots != P0.n_tslots) { lean_why(2); return 0; }
+    if (P0.tdt != P0.ddt || (P0.tdt != SD_BF16 && P0.tdt != SD_F16)) { lean_why(3); return 0; }
+    if (P0.n_tslots > sd::kLeanMaxT || P0.B > kCntMax || !poll_allowed()) { lean_why(4); return 0; }
+    int mode = -1;
+    if (const char* e = getenv("SD_LEAN_VERIFY")) mode = atoi(e);
+    if (mode == 0 || (mode < 0 && P0.B > kLeanVerifyMaxB)) { lean_why(5); return 0; }
+    constexpr int kSpan = kThreads * 8;
+    const int n_span = (P0.V + kSpan - 1) / kSpan;
+    if (n_span > kWave || P0.rn_chunks != n_span || P0.rchunk != kSpan) { lean_why(6); return 0; }
+    if ((P0.tstride * 2) % 16 || (P0.dstride * 2) % 16) { lean_why(7); return 0; }
+    for (int t = 0; t < P0.n_tslots; ++t)
+        if (reinterpret_cast<uintptr_t>(P0.trow[t]) & 15) { lean_why(8); return 0; }
+    for (int t = 0; t < P0.gamma; ++t)
+        if (reinterpret_cast<uintptr_t>(P0.drow[t]) & 15) { lean_why(9); return 0; }
+    const bool fast = P0.tT == 1.0f && P0.dT == 1.0f;
+    const bool stoch = P0.t_stoch != 0;
+    const int di = P0.tdt == SD_BF16 ? 0 : 1;
+    using K = void (*)(sd::Plan);
+    static const K kerns[2][2][2] = {
+        {{sd::k_verify_lean<SD_BF16, false, false>, sd::k_verify_lean<SD_BF16, false, true>},
+         {sd::k_verify_lean<SD_BF16, true, false>, sd::k_verify_lean<SD_BF16, true, true>}},
+        {{sd::k_verify_lean<SD_F16, false, false>, sd::k_verify_lean<SD_F16, false, true>},
+         {sd::k_verify_lean<SD_F16, true, false>, sd::k_verify_lean<SD_F16, true, true>}}};
+    const K kern = kerns[di][fast][stoch];
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> caps;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) { lean_why(10); return 0; }
+    int cap;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = caps.find({dev, (const void*)kern});
+        if (it == caps.end()) {
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kThreads, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+                per_cu = cus = 0;
+            it = caps.emplace(std::make_pair(dev, (const void*)kern), per_cu * cus).first;
+        }
+        cap = it->second;
+    }
+    if ((int64_t)P0.B * n_span > cap) { lean_why(11); return 0; }
+    sd::Plan P = P0;
+    P.n_chunks = n_span;
+    P.chunk = kSpan;
+    P.stat_slots = P0.n_tslots;
+    P.kpoll = 1;
+    P.xcd_affine = 0;
+    // the statistics records after the sampler's (ResPart-sized) chunk records, 16-byte aligned;
+    // both fit the workspace's rpart region: B (2γ+1) (nc+1) ResParts >= B n_span (ResPart + 16 n_t)
+    const uintptr_t srec = reinterpret_cast<uintptr_t>(P0.rpart + (int64_t)P0.B * n_span);
+    P.srec = reinterpret_cast<uint4*>((srec + 15) & ~uintptr_t(15));
+    SD_LAUNCH(kern, dim3(n_span, P.B), dim3(kThreads), stream, P);
+    lean_why(0);
+    return 1;
 }
 
 // STREAM multinomial rows (T = 1, no processor, 16-bit, aligned) in one pass (k_draw_stream,
@@ -3356,6 +3468,10 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     if (const char* e = getenv("SD_DEC_IN_SAMPLE")) P.dec_in_sample = perf && P.tails && P.t_stoch && atoi(e);
     P.xcd_affine = perf && P.B % 8 == 0;
     if (const char* e = getenv("SD_XCD_AFFINE")) P.xcd_affine = P.xcd_affine && atoi(e);
+    if (!a->prof_stats_begin) {   // the batch-1 / few-sequence verify in one launch (sd_verify_lean.inc)
+        const int32_t st = launch_verify_lean(P, stream);
+        if (st) return st < 0 ? st : SD_OK;
+    }
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
     const int reps = a->prof_stats_begin && a->prof_stats_repeat > 1 ? a->prof_stats_repeat : 1;
     for (int rep = 0; rep < reps; ++rep)
