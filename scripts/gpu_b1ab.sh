@@ -5,7 +5,7 @@
 set -eo pipefail
 cd $GRAFT_REPO_ROOT
 T="python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu"
-timeout -k 10 300 $T tests/test_gpu_parity.py tests/test_gpu_perfmode.py tests/test_gpu_greedy.py tests/test_gpu_engine_surface.py > gpurun_out/b1_tests.log 2>&1
+timeout -k 10 300 $T tests/test_gpu_lean_verify.py tests/test_gpu_parity.py tests/test_gpu_perfmode.py tests/test_gpu_greedy.py tests/test_gpu_engine_surface.py tests/test_gpu_errors.py tests/test_gpu_threshold.py > gpurun_out/b1_tests.log 2>&1
 timeout -k 10 300 python scripts/b1_ab.py "" $AB > gpurun_out/b1_ab.txt 2>&1
 if [ -n "$LIB2" ]; then
   SPECDEC_LIB=$LIB2 timeout -k 10 300 python scripts/b1_ab.py "" $AB > gpurun_out/b1_ab_lib2.txt 2>&1

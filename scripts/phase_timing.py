@@ -60,8 +60,8 @@ for rep in range(3):
     print(f"--- rep {rep}")
     for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "merged", "arrived", "decided", "dec_stats", "dec_ratios",
                                                         "stream_done", "pf_late", "rec_stored"]
-                   if not LEAN else ["start", "merged", "rec_stored", "decided", "dec_stats", "dec_ratios",
-                                     "loads_landed", "rows_reduced", "pf_late", "poll_1st", "-", "poll_done"]),
+                   if not LEAN else ["start", "merged", "rec_stored", "decided", "accepts", "-",
+                                     "loads_landed", "rows_reduced"]),
                                  ("k_sample_finish", 16384 - 64, 16384, ["start", "prologue", "body_end", "arrived",
                                                             "tail_S", "cdf_pick", "finalized", "cdf_select",
                                                             "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"]),

@@ -937,6 +937,66 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
     q = round_dyn(P.ddt, sd_exp(yd - msd.x) / msd.y);
 }
 
+// The perf-mode walk (walk_core's rules) from two ballots over the drafts' accept and stop flags
+// (wave 0; lane 0 builds the Decision, carrying the sampled rows' (m, S) from lstat).
+__device__ __forceinline__ void walk_decision(const Plan& P, int b, const uint8_t* lacc, const uint8_t* lstop, bool act,
+                                              const float2* lstat, Decision* out, bool publish) {
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < kWave) {
+        const int g = P.gamma;
+        const bool in = lane < g;
+        const bool acc = in && lacc[lane] != 0;
+        const uint64_t rejm = __ballot(in && !acc), stopm = __ballot(in && lstop[lane] != 0);
+        const int f_rej = rejm ? __builtin_ctzll(rejm) : g;             // first rejected draft (g: none)
+        const uint64_t before = f_rej >= 64 ? ~0ull : ((1ull << f_rej) - 1ull);
+        const uint64_t stop_acc = stopm & before;                        // stop tokens among the accepted
+        if (lane != 0) return;
+        Decision d{};
+        d.stop_index = -1;
+        d.noise_off = 0;
+        if (P.rule == SD_RULE_SPEC) {
+            d.n = f_rej;
+            if (stop_acc) {
+                d.stop_index = __builtin_ctzll(stop_acc);
+                d.mode = kModeNone;
+                d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
+            } else {
+                if (f_rej == g) { d.mode = kModeBonus; d.slot = g; d.status = SD_ROW_DONE | SD_ROW_BONUS; }
+                else if (P.skip_adj) { d.mode = kModePRow; d.slot = f_rej; d.status = SD_ROW_DONE | SD_ROW_FALLBACK_P; }
+                else { d.mode = kModeResid; d.slot = f_rej; d.status = SD_ROW_DONE | SD_ROW_RESIDUAL; }
+                d.noise_off = g;
+            }
+        } else {
+            d.mode = kModeNone;
+            d.n = 0;
+            if (act) {
+                d.status = SD_ROW_DONE;
+                if (stop_acc) {
+                    d.n = __builtin_ctzll(stop_acc) + 1;
+                    d.status |= SD_ROW_FINISHED;
+                } else if (f_rej < g) {
+                    d.n = f_rej;
+                    d.mode = kModeResid;
+                    d.slot = f_rej;
+                    d.status |= SD_ROW_RESIDUAL;
+                    d.noise_off = f_rej + 1;
+                } else {
+                    d.n = g;
+                }
+            }
+        }
+        if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision
+            d.mst = lstat[d.slot];
+            d.msd = d.mode == kModeResid && !P.draft_is_probs ? lstat[P.n_tslots + d.slot] : make_float2(0.f, 1.f);
+        }
+        if (out) *out = d;
+        if (publish) {
+            publish_decision(P, b, d);
+            if (P.words_used && b == 0) *P.words_used = 0;
+        }
+    }
+}
+
 // Perf-mode decision of sequence b by one 256-thread workgroup (the k_stats tail, or every k_sample
 // workgroup of the sequence when the decision is replicated there: out = its LDS copy, publish only
 // from one of them): row stats
@@ -1034,60 +1094,7 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
         __syncthreads();
         SD_TS(wg_id, 5);
     }
-    // the walk (walk_core's rules) from two ballots over the drafts' flags
-    if (threadIdx.x < kWave) {
-        const int g = P.gamma;
-        const bool in = lane < g;
-        const bool acc = in && lacc[lane] != 0;
-        const uint64_t rejm = __ballot(in && !acc), stopm = __ballot(in && lstop[lane] != 0);
-        const int f_rej = rejm ? __builtin_ctzll(rejm) : g;             // first rejected draft (g: none)
-        const uint64_t before = f_rej >= 64 ? ~0ull : ((1ull << f_rej) - 1ull);
-        const uint64_t stop_acc = stopm & before;                        // stop tokens among the accepted
-        if (lane != 0) return;
-        Decision d{};
-        d.stop_index = -1;
-        d.noise_off = 0;
-        if (P.rule == SD_RULE_SPEC) {
-            d.n = f_rej;
-            if (stop_acc) {
-                d.stop_index = __builtin_ctzll(stop_acc);
-                d.mode = kModeNone;
-                d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
-            } else {
-                if (f_rej == g) { d.mode = kModeBonus; d.slot = g; d.status = SD_ROW_DONE | SD_ROW_BONUS; }
-                else if (P.skip_adj) { d.mode = kModePRow; d.slot = f_rej; d.status = SD_ROW_DONE | SD_ROW_FALLBACK_P; }
-                else { d.mode = kModeResid; d.slot = f_rej; d.status = SD_ROW_DONE | SD_ROW_RESIDUAL; }
-                d.noise_off = g;
-            }
-        } else {
-            d.mode = kModeNone;
-            d.n = 0;
-            if (pf.act) {
-                d.status = SD_ROW_DONE;
-                if (stop_acc) {
-                    d.n = __builtin_ctzll(stop_acc) + 1;
-                    d.status |= SD_ROW_FINISHED;
-                } else if (f_rej < g) {
-                    d.n = f_rej;
-                    d.mode = kModeResid;
-                    d.slot = f_rej;
-                    d.status |= SD_ROW_RESIDUAL;
-                    d.noise_off = f_rej + 1;
-                } else {
-                    d.n = g;
-                }
-            }
-        }
-        if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision
-            d.mst = lstat[d.slot];
-            d.msd = d.mode == kModeResid && !P.draft_is_probs ? lstat[P.n_tslots + d.slot] : make_float2(0.f, 1.f);
-        }
-        if (out) *out = d;
-        if (publish) {
-            publish_decision(P, b, d);
-            if (P.words_used && b == 0) *P.words_used = 0;
-        }
-    }
+    walk_decision(P, b, lacc, lstop, pf.act, lstat, out, publish);
 }
 
 // grid (B): decide_seq as its own launch (perf mode without the k_stats tail)
@@ -3127,15 +3134,17 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
 constexpr int kLeanVerifyMaxB = 8;
 
 static void lean_why(int k) {
-    static const bool dbg = getenv("SD_LEAN_DEBUG") != nullptr;
+    const bool dbg = getenv("SD_LEAN_DEBUG") != nullptr;   // read per call: tests flip it
     if (dbg) fprintf(stderr, k ? "launch_verify_lean: not applicable (%d)\n" : "launch_verify_lean: launched\n", k);
 }
 
 int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
     if (P0.noise.mode == SD_NOISE_STREAM || !P0.tails || P0.dec_in_sample) { lean_why(1); return 0; }
-    if (P0.t_keep || P0.d_keep || !P0.dstats || P0.draft_is_probs || P0.stat_slots != P0.n_tslots) { lean_why(2); return 0; }
+    // statistics: the target rows with the draws' drafter stats, or every row here; keep
+    // predicates from this call's threshold search (P.keep) or the draws' (P.dkeep)
+    if (P0.draft_is_probs || P0.stat_slots != (P0.dstats ? P0.n_tslots : P0.slots)) { lean_why(2); return 0; }
     if (P0.tdt != P0.ddt || (P0.tdt != SD_BF16 && P0.tdt != SD_F16)) { lean_why(3); return 0; }
-    if (P0.n_tslots > sd::kLeanMaxT || P0.B > kCntMax || !poll_allowed()) { lean_why(4); return 0; }
+    if (P0.n_tslots > sd::kLeanMaxT || P0.gamma > SD_LEAN_MAX_GAMMA || P0.B > kCntMax || !poll_allowed()) { lean_why(4); return 0; }
     int mode = -1;
     if (const char* e = getenv("SD_LEAN_VERIFY")) mode = atoi(e);
     if (mode == 0 || (mode < 0 && P0.B > kLeanVerifyMaxB)) { lean_why(5); return 0; }
@@ -3147,7 +3156,7 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
         if (reinterpret_cast<uintptr_t>(P0.trow[t]) & 15) { lean_why(8); return 0; }
     for (int t = 0; t < P0.gamma; ++t)
         if (reinterpret_cast<uintptr_t>(P0.drow[t]) & 15) { lean_why(9); return 0; }
-    const bool fast = P0.tT == 1.0f && P0.dT == 1.0f;
+    const bool fast = P0.tT == 1.0f && P0.dT == 1.0f && !P0.t_keep && !P0.d_keep;
     const bool stoch = P0.t_stoch != 0;
     const int di = P0.tdt == SD_BF16 ? 0 : 1;
     using K = void (*)(sd::Plan);
@@ -3167,7 +3176,7 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
         auto it = caps.find({dev, (const void*)kern});
         if (it == caps.end()) {
             int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, kThreads, 0) != hipSuccess ||
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, sd::kLeanThreads, 0) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
                 per_cu = cus = 0;
             it = caps.emplace(std::make_pair(dev, (const void*)kern), per_cu * cus).first;
@@ -3178,14 +3187,13 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
     sd::Plan P = P0;
     P.n_chunks = n_span;
     P.chunk = kSpan;
-    P.stat_slots = P0.n_tslots;
     P.kpoll = 1;
     P.xcd_affine = 0;
     // the statistics records after the sampler's (ResPart-sized) chunk records, 16-byte aligned;
-    // both fit the workspace's rpart region: B (2γ+1) (nc+1) ResParts >= B n_span (ResPart + 16 n_t)
+    // both fit the workspace's rpart region: B (2γ+1) (nc+1) ResParts >= B n_span (ResPart + 16 (2γ+1))
     const uintptr_t srec = reinterpret_cast<uintptr_t>(P0.rpart + (int64_t)P0.B * n_span);
     P.srec = reinterpret_cast<uint4*>((srec + 15) & ~uintptr_t(15));
-    SD_LAUNCH(kern, dim3(n_span, P.B), dim3(kThreads), stream, P);
+    SD_LAUNCH(kern, dim3(n_span, P.B), dim3(sd::kLeanThreads), stream, P);
     lean_why(0);
     return 1;
 }
