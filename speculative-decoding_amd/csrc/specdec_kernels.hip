@@ -217,15 +217,19 @@ struct FSum {
     __device__ float operator()(float a, float b) const { return a + b; }
 };
 
+// Block reductions over the workgroup's waves: nw > 0 names the waves that take part (the
+// sampling bodies run in k_verify_lean's four data waves after its helper wave has exited, so
+// blockDim would count one wave too many), else every wave of the launch.
 template <typename F>
-__device__ __forceinline__ float block_reduce(float v, F op, float* lds) {
+__device__ __forceinline__ float block_reduce(float v, F op, float* lds, int nw = 0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     v = wave_reduce(v, F::kId, op);
     __syncthreads();
     if (lane == 0) lds[w] = v;
     __syncthreads();
     float r = lds[0];
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) r = op(r, lds[k]);
+    const int n = nw > 0 ? nw : (int)(blockDim.x >> 6);
+    for (int k = 1; k < n; ++k) r = op(r, lds[k]);
     return r;
 }
 
@@ -242,14 +246,15 @@ __device__ __forceinline__ float2 block_reduce2(float2 v, float* lds) {
     return r;
 }
 
-__device__ __forceinline__ void block_argmax(float& v, int32_t& i, float* ldsv, int32_t* ldsi) {
+__device__ __forceinline__ void block_argmax(float& v, int32_t& i, float* ldsv, int32_t* ldsi, int nw = 0) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     wave_argmax(v, i);
     __syncthreads();
     if (lane == 0) { ldsv[w] = v; ldsi[w] = i; }
     __syncthreads();
     v = ldsv[0]; i = ldsi[0];
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k)
+    const int n = nw > 0 ? nw : (int)(blockDim.x >> 6);
+    for (int k = 1; k < n; ++k)
         if (arg_better(ldsv[k], ldsi[k], v, i)) { v = ldsv[k]; i = ldsi[k]; }
 }
 
@@ -1248,8 +1253,8 @@ __device__ __forceinline__ void resid_body(const Plan& P, const Decision& d, int
             wmax = fmaxf(wmax, stoch ? rr * __builtin_amdgcn_rcpf(e[k]) : rr);
         }
     }
-    const float bsum = block_reduce(sum, FSum(), ldsf);
-    const float bw = block_reduce(wmax, FMax(), ldsf);
+    const float bsum = block_reduce(sum, FSum(), ldsf, kThreads / kWave);
+    const float bw = block_reduce(wmax, FMax(), ldsf, kThreads / kWave);
     if (threadIdx.x == 0) lcount = 0;
     __syncthreads();
     // any j whose exact fl(fl(res/S)/E) can tie the maximum has res/E within a few ulp of it
@@ -1362,7 +1367,7 @@ __device__ __forceinline__ void prow_body(const Plan& P, const Decision& d, int 
             if (arg_better(val, (int32_t)j, pv, pi)) { pv = val; pi = (int32_t)j; }
         }
     }
-    block_argmax(pv, pi, ldsf, ldsi);
+    block_argmax(pv, pi, ldsf, ldsi, kThreads / kWave);
     if (threadIdx.x == 0) {
         ResPart& o = P.rpart[(int64_t)b * P.rn_chunks + c];
         st_coh(&o.pval, pv);
@@ -1411,7 +1416,8 @@ __device__ __forceinline__ void pick_wave(const Plan& P, int b, const Decision& 
         const int rt = b * P.slots + d.slot;
         const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
         const void* trow = static_cast<const char*>(P.trow[d.slot]) + b * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
-        const float2 mst = P.rowstat[rt];
+        const float2 mst = d.mst;   // the decision carries the rows' (m, S): no read of rowstat, which
+                                    // k_verify_lean writes in this same launch
         if (P.rule == SD_RULE_ENGINE && (double)s <= 1e-12) {
             // engine/infer_engine.py:319-321: multinomial(p) over the target row (rare: p ~= q)
             float bv = -INFINITY;
@@ -1459,7 +1465,7 @@ __device__ __forceinline__ void pick_wave(const Plan& P, int b, const Decision& 
                     const int rd = b * P.slots + P.n_tslots + d.slot;
                     drow = static_cast<const char*>(P.drow[d.slot]) + b * P.dstride * (P.ddt == SD_F32 ? 4 : 2);
                     if (P.d_keep) kd = keep_of(P, rd);
-                    msd = P.rowstat[rd];
+                    msd = d.msd;
                     ddt = P.ddt;
                 }
                 for (int64_t j = lane; j < P.V; j += kWave) {
@@ -1489,7 +1495,7 @@ __device__ __forceinline__ void pick_wave(const Plan& P, int b, const Decision& 
         x = pi;
         // multinomial over a row whose softmax is NaN / inf (a NaN or +inf logit): torch raises
         // (utils/logits_processor.py:48-49); torch.argmax (greedy) does not
-        const float2 ms = P.rowstat[b * P.slots + d.slot];
+        const float2 ms = d.mst;
         if (P.t_stoch && !(ms.y > 0.f && ms.y < INFINITY)) status |= SD_ROW_INVALID_DIST;
     }
 }
@@ -2721,19 +2727,25 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         }
         return;
     }
-    // span pick: first span whose fp64 running total (span order) exceeds u * Σ
-    double base_d = 0.0, tot = 0.0;
+    // span pick: first span whose fp64 running total (span order) exceeds u * Σ.  One fp64 scan
+    // per pass (reused for the total), and only the passes the row has (one for V <= 128 Ki)
+    double sincl[2] = {0.0, 0.0};
+    double tot = 0.0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) tot += lane_d(wave_incl_scan_d((double)wk[q]), 63);
+    for (int q = 0; q < 2; ++q) {
+        if (q < npass) {
+            sincl[q] = tot + wave_incl_scan_d((double)wk[q]);
+            tot = lane_d(sincl[q], 63);
+        }
+    }
     const double tt = u_row * tot;
     int pick = -1, lastpos = -1;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-        const double incl2 = base_d + wave_incl_scan_d((double)wk[q]);
-        const uint64_t hit = __ballot(incl2 > tt && wk[q] > 0.f), posm = __ballot(wk[q] > 0.f);
+        if (q >= npass) break;
+        const uint64_t hit = __ballot(sincl[q] > tt && wk[q] > 0.f), posm = __ballot(wk[q] > 0.f);
         if (pick < 0 && hit) pick = q * kWave + __builtin_ctzll(hit);
         if (posm) lastpos = q * kWave + 63 - __builtin_clzll(posm);
-        base_d = lane_d(incl2, 63);
     }
     if (pick < 0) pick = lastpos;   // rounding left t at / after the total: the last positive span
     int32_t x = -1;
