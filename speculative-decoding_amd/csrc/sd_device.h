@@ -562,6 +562,13 @@ __device__ __forceinline__ float exp1_from_word(uint32_t w) {
     return -__logf(u);
 }
 
+// perf-mode span race of row `row` (k_draw_lean): Gumbel noise g_c = -ln E_c of span c from word z of
+// the span's cdf block (words x, y are its in-span uniform, cdf_uniform(row, 1 + c)); the row's span
+// is argmax_c (m_c + ln S_c + g_c), i.e. span c with probability S_c e^(m_c) / Σ (Gumbel-max)
+__device__ __forceinline__ float span_gumbel(const sd_noise& nz, uint32_t row, uint32_t c) {
+    return -__logf(exp1_from_word(philox_block(nz, row, kSiteCdf, 1u + c).z));
+}
+
 // Exp(1) noise of element j of a sampled row.  STREAM: torch's exponential_ draw for element j
 // (2 words at woff + 2j).  PHILOX: word (j & 3) of block (row, sample, j >> 2).
 __device__ __forceinline__ float exp_noise(const sd_noise& nz, int64_t woff, int row, int64_t j) {

@@ -779,6 +779,11 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
     if (overrun || (P.noise.mode == SD_NOISE_STREAM && d.mode != kModeNone && P.t_stoch &&
                     d.noise_off + sample_words > P.noise.n_words))
         d.status |= SD_ROW_NOISE_OVERRUN;
+    if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision (pick_wave reads them)
+        d.mst = P.rowstat[b * P.slots + d.slot];
+        d.msd = d.mode == kModeResid && !P.draft_is_probs ? P.rowstat[b * P.slots + P.n_tslots + d.slot]
+                                                          : make_float2(0.f, 1.f);
+    }
     *used_out = used;
     return d;
 }
@@ -2613,7 +2618,19 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     int32_t jk[2];
     bool dk[2] = {false, false};   // GREEDY: the span's dirty flag
     const int npass = (A.n_span + kWave - 1) / kWave;   // <= 2 (host: n_span <= 128)
+#ifdef SD_DRAW_CDF_PICK
     const double u_row = GREEDY ? 0.0 : cdf_uniform(A.noise, (uint32_t)r);   // scalar unit, before the wait
+#else
+    // the span race's Gumbel noise, one span per lane and pass, before the wait (off the chain)
+    float gk[2] = {0.f, 0.f};
+    if constexpr (!GREEDY) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int k = q * kWave + lane;
+            if (q < npass && k < A.n_span) gk[q] = span_gumbel(A.noise, (uint32_t)r, (uint32_t)k);
+        }
+    }
+#endif
     if (A.poll) {
         // every other span's record, re-read until its tag is this launch's; this span's own from
         // registers (the lane that would hold it)
@@ -2727,6 +2744,26 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         }
         return;
     }
+#ifndef SD_DRAW_CDF_PICK
+    // span pick by a Gumbel race: argmax_c (m_c + ln S_c + g_c) picks span c with probability
+    // S_c e^(m_c) / Σ — independent of M and S, so its wave max runs beside theirs (no fp64 scan)
+    float key[2];
+    float kmax = -INFINITY;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        key[q] = mk[q] > -INFINITY && sk[q] > 0.f ? mk[q] + __logf(sk[q]) + gk[q] : -INFINITY;
+        kmax = fmaxf(kmax, key[q]);
+    }
+    kmax = wave_max(kmax);
+    int pick = -1;
+    if (kmax > -INFINITY) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint64_t hit = __ballot(key[q] == kmax);
+            if (pick < 0 && hit) pick = q * kWave + __builtin_ctzll(hit);
+        }
+    }
+#else
     // span pick: first span whose fp64 running total (span order) exceeds u * Σ.  One fp64 scan
     // per pass (reused for the total), and only the passes the row has (one for V <= 128 Ki)
     double sincl[2] = {0.0, 0.0};
@@ -2748,6 +2785,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         if (posm) lastpos = q * kWave + 63 - __builtin_clzll(posm);
     }
     if (pick < 0) pick = lastpos;   // rounding left t at / after the total: the last positive span
+#endif
     int32_t x = -1;
     float yx = -INFINITY;
     if (pick >= 0) {
