@@ -2422,6 +2422,21 @@ __device__ __forceinline__ uint32_t draw_tag(uint32_t epoch, int r, int c, int n
 // its normaliser is not finite (NaN / inf logits).
 constexpr float kGreedyDelta = 1.0f / 32.0f;
 
+// k_draw_lean A/B switches of the build.  SD_DRAW_PUB_CLAIM=1: the claiming wave publishes the
+// span's record itself, no second barrier (measured slower: 6.8 vs 6.5 us per bench draw, the
+// claiming wave is rarely wave 0).  SD_DRAW_POLL2=1: two staggered polls in flight (measured slower:
+// 7.2 vs 6.65 us per bench draw, 5.0 vs 4.5 at batch 1 — the row's last span is dispatched last and
+// usually finds every record at its first poll, so the stagger only delays it).
+#ifndef SD_DRAW_PUB_CLAIM
+#define SD_DRAW_PUB_CLAIM 0
+#endif
+#ifndef SD_DRAW_POLL2
+#define SD_DRAW_POLL2 0
+#endif
+#ifndef SD_DRAW_STAGGER
+#define SD_DRAW_STAGGER 8   // the second poll's delay, in s_sleep units of 64 clocks
+#endif
+
 template <int DT, int NST>
 __device__ int greedy_rescan(const DrawLean& A, const char* row, int c, float M, float S) {
     constexpr int VEC = 8, STEP = kThreads * VEC, SPAN = NST * STEP, PER = SPAN / kWave;
@@ -2482,11 +2497,15 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     __shared__ int32_t l_j;
     __shared__ float l_y;
     __shared__ int32_t l_fi[NW], l_dirty[NW];
+    __shared__ uint32_t l_epoch;
     uint32_t epoch = 0;   // poll mode: this launch's epoch of row r (read by wave 0, beside the loads)
     if (w == 0) {   // the span's in-chunk uniform: one wave's scalar unit, while the loads fly
         if (A.poll) epoch = __hip_atomic_load(seq_counter(A.cnt, 2, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double u = GREEDY ? 0.0 : cdf_uniform(A.noise, (uint32_t)r, 1u + (uint32_t)c);
-        if (lane == 0) { l_u = u; l_j = -1; l_y = -INFINITY; }
+        if (lane == 0) {
+            l_u = u; l_j = -1; l_y = -INFINITY;
+            if constexpr (!GREEDY && SD_DRAW_PUB_CLAIM) l_epoch = epoch;   // (waits for the epoch load)
+        }
     }
     // per-wave max and weights: no barrier before the exps
     float mv = y[0];
@@ -2511,12 +2530,14 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     for (int k = 1; k < NW; ++k) m = fmaxf(m, l_m[k]);
     float off = 0.f, my_off = 0.f, my_sc = 0.f, my_W = 0.f;
     int lastw = -1;
+    float l_off[NW], l_W[NW];   // (registers) every wave's offset and weight
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
         const float sc = l_m[k] > -INFINITY ? __builtin_amdgcn_exp2f((l_m[k] - m) * kLog2e) : 0.f;
         const float Wk = l_s[k] * sc;
         if (k == w) { my_off = off; my_sc = sc; my_W = Wk; }
         if (Wk > 0.f) lastw = k;
+        l_off[k] = off; l_W[k] = Wk;
         off += Wk;
     }
     const float T = off;
@@ -2536,13 +2557,22 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         if (lane == 0) { l_fi[w] = fi; l_dirty[w] = dw; }
     }
     const float t = (float)(l_u * (double)T);
-    // the claiming wave (rounding past the end: the last wave with weight)
-    const bool claim = !GREEDY && my_W > 0.f &&
-                       ((t >= my_off && t < my_off + my_W) || (w == lastw && t >= my_off + my_W));
+    // the claiming wave (rounding past the end: the last wave with weight); every thread knows it
+    int cw = -1;
+#pragma unroll
+    for (int k = 0; k < NW; ++k)
+        if (cw < 0 && l_W[k] > 0.f &&
+            ((t >= l_off[k] && t < l_off[k] + l_W[k]) || (k == lastw && t >= l_off[k] + l_W[k])))
+            cw = k;
+    const bool claim = !GREEDY && cw == w;
+    (void)my_W;
+    int32_t cj = -1;   // the claiming lane's element and its logit
+    float cy = -INFINITY;
+    int hl = -1;
     if (claim) {
         const float a = fmaf(incl, my_sc, my_off), a0 = lane == 0 ? my_off : fmaf(prev, my_sc, my_off);
         const uint64_t hit = __ballot(a > t && tl > 0.f), posm = __ballot(tl > 0.f);
-        const int hl = hit ? __builtin_ctzll(hit) : (posm ? 63 - __builtin_clzll(posm) : -1);
+        hl = hit ? __builtin_ctzll(hit) : (posm ? 63 - __builtin_clzll(posm) : -1);
         if (lane == hl) {
             float run = a0;
             int kk = -1, lastk = -1;
@@ -2560,18 +2590,31 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
                 float yk = y[0];
 #pragma unroll
                 for (int k = 1; k < EPT; ++k) yk = k == kk ? y[k] : yk;
-                l_j = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + (kk - v * VEC));
-                l_y = yk;
+                cj = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + (kk - v * VEC));
+                cy = yk;
             }
         }
     }
-    __syncthreads();
-    SD_TSL(ts_wg, 2);
-    if (w != 0) return;
+    constexpr bool kPub = !GREEDY && SD_DRAW_PUB_CLAIM;
+    if constexpr (kPub) {
+        // the claiming wave publishes and (last span) runs the tail: no second barrier; wave 0 when
+        // no wave claims (a span of zero or NaN weight)
+        if (w != (cw >= 0 ? cw : 0)) return;
+        if (hl >= 0) {
+            cj = __builtin_amdgcn_readlane(cj, hl);
+            cy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), hl));
+        }
+        epoch = l_epoch;
+    } else {
+        if (claim && lane == hl) { l_j = cj; l_y = cy; }
+        __syncthreads();
+        SD_TSL(ts_wg, 2);
+        if (w != 0) return;
+    }
     const bool bad = T != T;   // NaN / +inf in the span: S_c NaN flags the row
     const float m_pub = bad && !(m > -INFINITY) ? 0.f : m, s_pub = bad ? NAN : T;
-    int32_t j_pub = l_j;
-    float y_pub = l_y;
+    int32_t j_pub = kPub ? cj : l_j;
+    float y_pub = kPub ? cy : l_y;
     int32_t g_dirty = 0;   // GREEDY: another value within kGreedyDelta of the span max
     if constexpr (GREEDY) {
         j_pub = l_fi[0];
@@ -2589,7 +2632,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         // the tail and advances the row's epoch.  No counter, no write-ack wait on the path.
         const uint32_t tag = draw_tag(epoch, r, c, A.n_span);
         if (c != A.n_span - 1) {
-            if (threadIdx.x == 0) {
+            if (lane == 0) {
                 const uint32_t yraw = DT == SD_BF16 ? (__float_as_uint(y_pub) >> 16)
                                                     : (uint32_t)__half_as_ushort(__float2half_rn(y_pub));
                 const uint32_t off = j_pub >= 0 ? (uint32_t)(j_pub - base) + 1u : 0u;   // <= NST * 2048
@@ -2603,7 +2646,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         // counter mode (many rows: more consumers than resident workgroups could spin): thread 0
         // publishes {m_c, S_c, j_c, y_{j_c}} and arrives; the last arrival runs the tail
         uint32_t last = 0;
-        if (threadIdx.x == 0) {
+        if (lane == 0) {
             st_coh16(part_row + c, make_uint4(__float_as_uint(m_pub), __float_as_uint(s_pub), (uint32_t)j_pub,
                                               GREEDY ? (uint32_t)g_dirty : __float_as_uint(y_pub)));
             last = arrive_last(seq_counter(A.cnt, 0, r), (uint32_t)A.n_span) ? 1u : 0u;
@@ -2642,6 +2685,45 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             have[q] = !(q < npass && k < A.n_span) || k == c;
             rec[q] = make_uint4(0u, 0u, 0u, 0u);
         }
+#if SD_DRAW_POLL2
+        // Two polls in flight, staggered: a record that lands just after one poll's read is seen by
+        // the other about half a round trip later instead of a whole one.  The tags are computed
+        // before the wait (off the chain); each poll's loads are waited on separately.
+        uint32_t tg[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) tg[q] = draw_tag(epoch, r, q * kWave + lane, A.n_span);
+        uint4 ra[2], rb[2];
+        const bool live = A.spin_limit >= 0;   // < 0: the test hook, every record counts as lost
+        if (live) {
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                if (!have[q]) ra[q] = ld_coh16(pr + 2 * (q * kWave + lane));
+            __builtin_amdgcn_s_sleep(SD_DRAW_STAGGER);
+        }
+        for (int spin = 0;; ++spin) {
+            if (live) {
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (!have[q]) rb[q] = ld_coh16(pr + 2 * (q * kWave + lane));
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (!have[q] && ra[q].w == tg[q]) { have[q] = true; rec[q] = ra[q]; }
+                if (__all(have[0] && have[1])) break;
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (!have[q]) ra[q] = ld_coh16(pr + 2 * (q * kWave + lane));
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    if (!have[q] && rb[q].w == tg[q]) { have[q] = true; rec[q] = rb[q]; }
+                if (__all(have[0] && have[1])) break;
+            }
+            if (!spin_more(spin, A.spin_limit)) {   // bounded: ~tens of ms; the row is flagged, never a hang
+                xstat = SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#else
         for (int spin = 0;; ++spin) {
             if (A.spin_limit >= 0) {   // < 0: the test hook, every record counts as lost
 #pragma unroll
@@ -2659,6 +2741,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
+#endif
         SD_TSL(ts_wg, 4);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
