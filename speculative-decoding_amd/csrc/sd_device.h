@@ -405,6 +405,23 @@ __device__ __forceinline__ int wave_reduce_i(int v, int id, Op op) {
 __device__ __forceinline__ float wave_max(float v) {
     return wave_reduce(v, -INFINITY, [](float a, float b) { return fmaxf(a, b); });
 }
+// wave max on order-preserving integer keys (k_draw_lean's hot path): v_max_i32 needs no NaN
+// canonicalisation, so each step is one DPP-fused instruction instead of four.  A NaN input may win
+// or lose the max (fmaxf drops it); the callers flag such rows from their NaN weights either way.
+__device__ __forceinline__ float wave_max_ord(float v) {
+    int k = __float_as_int(v);
+    k ^= (k >> 31) & 0x7fffffff;
+    auto mx = [](int a, int b) { return a > b ? a : b; };
+    k = mx(k, dpp_i<kDppQuad1032>(INT_MIN, k));
+    k = mx(k, dpp_i<kDppQuad2301>(INT_MIN, k));
+    k = mx(k, dpp_i<kDppRowHalfMirror>(INT_MIN, k));
+    k = mx(k, dpp_i<kDppRowMirror>(INT_MIN, k));
+    k = mx(k, dpp_i<kDppRowBcast15, 0xA>(INT_MIN, k));
+    k = mx(k, dpp_i<kDppRowBcast31, 0xC>(INT_MIN, k));
+    k = lane63_i(k);
+    k ^= (k >> 31) & 0x7fffffff;
+    return __int_as_float(k);
+}
 __device__ __forceinline__ float wave_sum(float v) {
     return wave_reduce(v, 0.f, [](float a, float b) { return a + b; });
 }

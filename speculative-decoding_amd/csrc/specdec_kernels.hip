@@ -2433,6 +2433,14 @@ constexpr float kGreedyDelta = 1.0f / 32.0f;
 #ifndef SD_DRAW_POLL2
 #define SD_DRAW_POLL2 0
 #endif
+#ifndef SD_DRAW_VALU_TRIM
+#define SD_DRAW_VALU_TRIM 1   // integer-key wave max, no per-element select (A/B: 0)
+#endif
+#if SD_DRAW_VALU_TRIM
+#define SD_DRAW_WMAX wave_max_ord   // the tail's maxima: finite or -inf records, never NaN
+#else
+#define SD_DRAW_WMAX wave_max
+#endif
 #ifndef SD_DRAW_STAGGER
 #define SD_DRAW_STAGGER 8   // the second poll's delay, in s_sleep units of 64 clocks
 #endif
@@ -2511,13 +2519,25 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     float mv = y[0];
 #pragma unroll
     for (int k = 1; k < EPT; ++k) mv = fmaxf(mv, y[k]);
+#if SD_DRAW_VALU_TRIM
+    // integer-key wave max; a wave of -inf entries subtracts 0 (its weights are exp2(-inf) = 0),
+    // so no per-element select, and a NaN entry always makes its own weight NaN (the span's S_c
+    // NaN flags the row)
+    const float mw = wave_max_ord(mv);
+    const float mws = mw > -INFINITY ? mw : 0.f;
+#else
     const float mw = wave_max(mv);
+#endif
     SD_TSL(ts_wg, 1);
     float wv[EPT];
     float tl = 0.f;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
+#if SD_DRAW_VALU_TRIM
+        wv[k] = __builtin_amdgcn_exp2f((y[k] - mws) * kLog2e);
+#else
         wv[k] = mw > -INFINITY ? __builtin_amdgcn_exp2f((y[k] - mw) * kLog2e) : 0.f;
+#endif
         tl += wv[k];
     }
     const float incl = wave_incl_scan(tl);             // lane order, relative to mw
@@ -2557,15 +2577,19 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         if (lane == 0) { l_fi[w] = fi; l_dirty[w] = dw; }
     }
     const float t = (float)(l_u * (double)T);
-    // the claiming wave (rounding past the end: the last wave with weight); every thread knows it
-    int cw = -1;
+    // the claiming wave (rounding past the end: the last wave with weight)
+    constexpr bool kPub = !GREEDY && SD_DRAW_PUB_CLAIM;
+    int cw = -1;   // kPub: every thread knows the claiming wave
+    if constexpr (kPub) {
 #pragma unroll
-    for (int k = 0; k < NW; ++k)
-        if (cw < 0 && l_W[k] > 0.f &&
-            ((t >= l_off[k] && t < l_off[k] + l_W[k]) || (k == lastw && t >= l_off[k] + l_W[k])))
-            cw = k;
-    const bool claim = !GREEDY && cw == w;
-    (void)my_W;
+        for (int k = 0; k < NW; ++k)
+            if (cw < 0 && l_W[k] > 0.f &&
+                ((t >= l_off[k] && t < l_off[k] + l_W[k]) || (k == lastw && t >= l_off[k] + l_W[k])))
+                cw = k;
+    }
+    const bool claim = !GREEDY && (kPub ? cw == w
+                                        : my_W > 0.f && ((t >= my_off && t < my_off + my_W) ||
+                                                         (w == lastw && t >= my_off + my_W)));
     int32_t cj = -1;   // the claiming lane's element and its logit
     float cy = -INFINITY;
     int hl = -1;
@@ -2595,7 +2619,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             }
         }
     }
-    constexpr bool kPub = !GREEDY && SD_DRAW_PUB_CLAIM;
     if constexpr (kPub) {
         // the claiming wave publishes and (last span) runs the tail: no second barrier; wave 0 when
         // no wave claims (a span of zero or NaN weight)
@@ -2772,7 +2795,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         M = fmaxf(M, mk[q]);
     }
     }
-    M = wave_max(M);
+    M = SD_DRAW_WMAX(M);
     float wk[2], S = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -2837,7 +2860,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         key[q] = mk[q] > -INFINITY && sk[q] > 0.f ? mk[q] + __logf(sk[q]) + gk[q] : -INFINITY;
         kmax = fmaxf(kmax, key[q]);
     }
-    kmax = wave_max(kmax);
+    kmax = SD_DRAW_WMAX(kmax);
     int pick = -1;
     if (kmax > -INFINITY) {
 #pragma unroll
