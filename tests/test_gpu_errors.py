@@ -209,3 +209,45 @@ def test_status_or_collects_only_error_bits():
     assert int(err.item()) == _lib.SD_ROW_INVALID_DIST
     with pytest.raises(ValueError):
         ops.sample_rows(x, ops.PLAIN_SOFTMAX, PhiloxNoise(seed=1), status_or=err.long())
+
+
+@pytest.mark.parametrize("block", [(5 * 2048, 512), (7 * 2048 + 1536, 512), (3 * 2048, 2048)])
+def test_nan_block_flags_like_a_nan_row(block):
+    """A run of NaN logits covering one wave's elements (or a whole span) of a 128256-wide row: the
+    one-pass draws flag the row in both noise modes (torch.multinomial raises on its NaN softmax),
+    and the batch-1 one-launch verify treats a target row with such a block exactly as a row that
+    is NaN throughout (its softmax is NaN either way)."""
+    from specdec_amd import PhiloxNoise, StreamNoise, _lib, ops
+    V, g = 128256, 4
+    gen = torch.Generator().manual_seed(5)
+    tl = (torch.randn(1, g + 1, V, generator=gen) * 3).to(torch.bfloat16)
+    dl = (tl[:, :g].float() + torch.randn(1, g, V, generator=gen)).to(torch.bfloat16)
+    tl, dl = tl.to(DEV), dl.to(DEV)
+    off, n = block
+    for noise in (PhiloxNoise(seed=3), StreamNoise(torch.Generator().manual_seed(3))):
+        x = torch.cat([dl[:, 0], dl[:, 1]]).contiguous()
+        x[0, off:off + n] = float("nan")
+        _, _, st = ops.sample_rows(x, ops.PLAIN_SOFTMAX, noise)
+        st = st.cpu()
+        assert st[0] & _lib.SD_ROW_INVALID_DIST, (type(noise).__name__, int(st[0]))
+        assert not st[1] & _lib.SD_ROW_ERROR_MASK, (type(noise).__name__, int(st[1]))
+
+    def run(trows):
+        stats = torch.empty(g, 1, 2, dtype=torch.float32, device=DEV)
+        ids = torch.empty(1, g, dtype=torch.long, device=DEV)
+        noise = PhiloxNoise(seed=9)
+        for d in range(g):
+            tok, _, _ = ops.sample_rows(dl[:, d], ops.PLAIN_SOFTMAX, noise, row_stats_out=stats[d])
+            ids[:, d] = tok
+        return ops.verify([trows[:, t] for t in range(g + 1)], [dl[:, d] for d in range(g)], ids,
+                          _lib.SD_RULE_SPEC, ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX,
+                          PhiloxNoise(seed=9, offset=noise.offset), draft_row_stats=stats)
+
+    for slot in (0, g):
+        tb, tw = tl.clone(), tl.clone()
+        tb[0, slot, off:off + n] = float("nan")
+        tw[0, slot, :] = float("nan")
+        a, b = run(tb), run(tw)
+        mask = _lib.SD_ROW_ERROR_MASK
+        assert int(a.row_status[0]) & mask == int(b.row_status[0]) & mask, (slot, int(a.row_status[0]), int(b.row_status[0]))
+        assert int(a.n_accepted[0]) == int(b.n_accepted[0]), slot
