@@ -13,8 +13,9 @@ no collective on the data path), so scaling is weak: every rank verifies its own
 
 value = output tokens (accepted drafts + resampled tokens, all ranks, counted exactly by the
 verify kernel itself: sd_verify_args.row_counts) / max-over-ranks wall time of the K timed steps.
-Steps run as hipGraph replays — the K steps are >= 5 back-to-back replays of one captured graph,
-each also timed by HIP events (median reported) — and noise is in-kernel Philox (perf mode).
+Steps run as hipGraph replays — G = --graph-steps steps (default 20) per captured graph, K/G replays per
+timed trial; --trials trials of exactly K steps (median reported), each replay also timed by HIP events —
+and noise is in-kernel Philox (perf mode).
 Also reported in the same line: acceptance rate (engine/metrics.py:123-129) over >= 200 untimed
 steps, per-kernel timings with the HBM roofline of the step's DOMINANT kernel (the largest
 per-step share; HIP events on the launch stream, algorithmic bytes = every logit row the kernel
@@ -64,9 +65,18 @@ def parse():
     ap.add_argument("--stream-steps", type=int, default=5, help="STREAM-mode (bit-exact noise) steps; 0 = skip")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] / configs[4] batch-1 lines")
     ap.add_argument("--no-shards", action="store_true", help="skip the 16 / 8 / 4-row shard lines")
+    ap.add_argument("--trials", type=int, default=5,
+                    help="timed trials of exactly --steps steps each (median reported)")
+    ap.add_argument("--profile-only", action="store_true",
+                    help="only the B-row engine step (no shards, configs[1]/[4], STREAM or CPU lines): every "
+                         "sd:: launch of the run has the headline shape, for rocprofv3 / PMC passes")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsing N ranks on fewer GPUs)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.profile_only:
+        a.no_cpu_baseline = a.no_configs1 = a.no_shards = True
+        a.stream_steps = 0
+    return a
 
 
 def log(*a):
@@ -148,6 +158,11 @@ class EngineStep:
     def draw(self, d):
         self.ops.sample_rows(self.drows[d], self.ops.PLAIN_SOFTMAX, self.noise, tokens_out=self.draft[:, d],
                              row_base=self.row0, row_stats_out=self.dstats[d] if self.stash else None)
+
+    def draw_rows(self, rows):
+        """A draw of the slot-0 drafts from other [B, V] rows (the roofline's rotating draw loop)."""
+        self.ops.sample_rows(rows, self.ops.PLAIN_SOFTMAX, self.noise, tokens_out=self.draft[:, 0],
+                             row_base=self.row0, row_stats_out=self.dstats[0] if self.stash else None)
 
     def draws(self):
         for d in range(self.g):
@@ -237,15 +252,20 @@ def main():
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
-    # the K timed steps: >= 5 replays of one captured graph (G steps each), event-timed one by one
-    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps, noise, g + 1, min_replays=5)
+    # the K timed steps: one captured graph of G steps (G = --graph-steps, dividing K), replayed K/G times
+    # per trial; --trials trials of exactly K steps, each bracketed by a barrier and a device sync, the
+    # median trial reported (every trial's tokens counted exactly by the verify kernel)
+    graph, outs, replays = graph_steps(step, args.steps, args.graph_steps, noise, g + 1)
     G = len(outs)
     step.read_counts()                                   # drop the warm-up / capture replay's counts
-    replay_ms = []
-    elapsed = timed_replays(graph, replays, dist, replay_ms)
+    replay_ms, trial_s = [], []
+    for _ in range(max(args.trials, 1)):
+        trial_s.append(timed_replays(graph, replays, dist, replay_ms))
+    elapsed = statistics.median(trial_s)
     counts = step.read_counts()                          # exact: every timed step's tokens
-    tokens_t, acc_t = int(counts[:, 1].sum()), counts[:, 0]
-    rsum_t, rcnt_t = positive_rate_sums(acc_t, g * args.steps)
+    n_trials = len(trial_s)
+    tokens_t, acc_t = int(counts[:, 1].sum()) / n_trials, counts[:, 0]
+    rsum_t, rcnt_t = positive_rate_sums(acc_t, g * args.steps * n_trials)
 
     # acceptance over a larger untimed sample (>= 200 steps of the same graph, fresh noise each)
     n_count = max(1, -(-max(200, args.steps) // G))
@@ -256,18 +276,23 @@ def main():
 
     # the verify alone (on the captured draws' outputs), for the per-phase breakdown
     vgraph, _, vrep = graph_steps(step.verify, args.steps, args.graph_steps)
-    verify_ms = timed_replays(vgraph, vrep, None) / args.steps * 1e3
+    verify_ms = statistics.median(timed_replays(vgraph, vrep, None) for _ in range(3)) / args.steps * 1e3
 
     elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens_t, "accepted": float(acc_t.sum()),
-                                          "drafted": B * g * args.steps, "rate_sum": rsum, "rate_cnt": rcnt,
+                                          "drafted": B * g * args.steps * n_trials, "rate_sum": rsum, "rate_cnt": rcnt,
                                           "rate_sum_t": rsum_t, "rate_cnt_t": rcnt_t,
                                           "accepted_c": float(counts_c[:, 0].sum()),
                                           "drafted_c": B * g * G * n_count}, dev, dist)
 
     # per-kernel timing (HIP events on the launch stream, back-to-back launches so the event pair's
     # own cost is amortised): k_draw (one per drafter draw), k_stats (sd_verify's prof hook, with its
-    # decide tail), and the rest of the verify (k_sample with its tail) by difference.
-    dgraph, _, _ = graph_steps(lambda: step.draw(0), PROF_REPEAT, PROF_REPEAT)   # launch-overhead free
+    # decide tail), and the rest of the verify (k_sample with its tail) by difference.  The draws cycle
+    # over 8 distinct [B, V] row sets (the 4 drafter and 4 target rows, 2x the 32 MiB of aggregate L2 at
+    # the bench shape), so each launch reads its rows from Infinity Cache / HBM as in the step, not from
+    # an L2 a back-to-back loop over one row set would keep hot.
+    rot = step.drows + step.trows
+    dgraph, _, _ = graph_steps(lambda it=iter(range(1 << 30)): step.draw_rows(rot[next(it) % len(rot)]),
+                               PROF_REPEAT, PROF_REPEAT)   # launch-overhead free
     draw_ms = kernel_events(dgraph.replay, 1, args.prof_steps) / PROF_REPEAT
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.prof_steps)]
     for e in ev:
@@ -281,7 +306,10 @@ def main():
     row_bytes = B * V * 2
     kernels = {
         # per launch: algorithmic bytes = each logit row the kernel must read, once
-        "k_draw": {"ms": draw_ms, "launches_per_step": g, "alg_bytes_per_launch": row_bytes},
+        "k_draw": {"ms": draw_ms, "launches_per_step": g, "alg_bytes_per_launch": row_bytes,
+                   "in_step_ms": (ms_per_step - verify_ms) / g,
+                   "note": "ms: 20 graph-replayed launches over 8 rotating row sets; in_step_ms: the step's "
+                           "draw phase / γ (kernel boundaries included)"},
         "k_stats": {"ms": stats_ms, "launches_per_step": 1, "alg_bytes_per_launch": g * row_bytes},
         "k_sample": {"ms": sample_ms, "launches_per_step": 1, "alg_bytes_per_launch": 2 * row_bytes,
                      "note": "verify minus k_stats (graph-timed); rows re-read from L2 / Infinity Cache"},
@@ -354,7 +382,8 @@ def main():
             "config": {"workload": "configs[2]: Llama-3-8B/3.2-1B logit shapes, engine step sampling path: "
                                    "γ drafter draws + verify (rule A10)",
                        "rows_per_gpu": args.batch, "global_batch": args.batch * world, "gamma": g, "vocab": V,
-                       "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G, "replays": replays},
+                       "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G, "replays_per_trial": replays,
+                       "trials": n_trials},
             # engine/metrics.py:123-129: mean of per-row acc/tot over the rows with a positive rate,
             # over >= 200 untimed steps of the same graph (the timed steps' own figure beside it)
             "acceptance_rate": tot["rate_sum"] / tot["rate_cnt"] if tot["rate_cnt"] else 0.0,
@@ -362,11 +391,13 @@ def main():
             "acceptance_steps": G * n_count,
             "acceptance_rate_timed": tot["rate_sum_t"] / tot["rate_cnt_t"] if tot["rate_cnt_t"] else 0.0,
             "tokens_timed": tot["tokens"],
-            "replays": {"count": replays, "steps_per_replay": G,
+            "replays": {"count": replays * n_trials, "steps_per_replay": G,
                         "ms_median": statistics.median(replay_ms), "ms_min": min(replay_ms),
                         "ms_max": max(replay_ms),
                         "ms_per_step_median": statistics.median(replay_ms) / G,
-                        "note": "HIP events between back-to-back replays of the captured steps (rank 0)"},
+                        "trial_ms_per_step": [t / args.steps * 1e3 for t in trial_s],
+                        "note": "HIP events between back-to-back replays of the captured steps (rank 0); "
+                                "trial_ms_per_step: each trial's wall time / K (the value uses the median)"},
             "roofline": {"bound": "hbm", "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": dk["frac"], "traffic": traffic,
                          "kernel": dominant, "kernel_ms": dk["ms"], "launches_per_step": dk["launches_per_step"],

@@ -37,7 +37,9 @@ def main():
                     continue
                 k = (row["Dispatch_Id"], row["Counter_Name"])
                 per[k] += float(row["Counter_Value"])   # sum over XCD/SE instances
-                names[row["Dispatch_Id"]] = short(row["Kernel_Name"])
+                g = row.get("Grid_Size") or "x".join(row.get(f"Grid_Size_{a}", "") or "" for a in "XYZ")
+                # one entry per (kernel, grid): launches of other shapes never mix into an average
+                names[row["Dispatch_Id"]] = short(row["Kernel_Name"]) + (f" grid={g}" if g.strip("x") else "")
         for (disp, ctr), v in per.items():
             acc[names[disp]][ctr].append(v)
     ctrs = sorted({c for k in acc.values() for c in k})

@@ -346,6 +346,13 @@ __device__ __forceinline__ float process_value(float x, int64_t j, float T, bool
     float v = x;
     if (has_keep && !(x > keep.tau || (x == keep.tau && j <= keep.tie_idx))) v = round_dt<DT>(kNegFill);
     if (T != 1.0f) v = round_dt<DT>(v / T);
+    // A NaN / +inf logit under a top-k / nucleus keep stays NaN whether the cut keeps it or not:
+    // torch's topk and sort rank NaN first and keep +inf, whose softmax is NaN (inf - inf), so the
+    // reference's processed row is NaN throughout (utils/logits_processor.py:59-63,73-81).  Every
+    // consumer of a processed row takes its (max, Σexp) over all of it, and a NaN element makes
+    // those NaN: the row then behaves exactly as a NaN row (draws flag SD_ROW_INVALID_DIST, accept
+    // ratios are NaN as the reference's).
+    if (has_keep && !(x <= 3.402823466e38f)) v = __builtin_nanf("");
     return v;
 }
 

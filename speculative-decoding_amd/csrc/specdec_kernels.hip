@@ -1628,11 +1628,7 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
     for (int k = 0; k < VEC; ++k) {
         const int64_t j = e0 + k;
         const float yt = FAST ? xt[k] : process_value<TDT>(xt[k], j, R.tT, R.t_keep, R.kt);
-#ifdef SD_EXACT_SAMPLE_PROB
-        const float p = prob_exact<TDT>(yt, R.mst.x, R.mst.y, R.t_inv);
-#else
         const float p = prob_fast<TDT>(yt, R.mst.x, R.t_inv);
-#endif
         float v = p;
         if (R.resid) {
             float q;
@@ -1640,11 +1636,7 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
                 q = xd[k];
             } else {
                 const float yd = FAST ? xd[k] : process_value<DDT>(xd[k], j, R.dT, R.d_keep, R.kd);
-#ifdef SD_EXACT_SAMPLE_PROB
-                q = prob_exact<DDT>(yd, R.msd.x, R.msd.y, R.d_inv);
-#else
                 q = prob_fast<DDT>(yd, R.msd.x, R.d_inv);
-#endif
             }
             const float diff = p - q;
             v = diff > 0.f ? diff : 0.f;
@@ -2124,6 +2116,10 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
         if (P.t_keep) st |= keep_of(P, r).flags;
         if (P.noise.mode == SD_NOISE_STREAM && P.t_stoch && 2ll * P.V * P.B > P.noise.n_words)
             st |= SD_ROW_NOISE_OVERRUN;
+        // no candidate at all (an all-NaN / all -inf row: the race's threshold is NaN) is an invalid
+        // distribution too; a failed row's token is -1, never an index a forward could be fed
+        if (pi < 0 || pi >= P.V) st |= SD_ROW_INVALID_DIST;
+        if (st & SD_ROW_INVALID_DIST) pi = -1;
         P.next_token[r * P.next_token_stride] = pi;
         if (P.token_prob) {
             const void* row = static_cast<const char*>(P.trow[0]) + r * P.tstride * (P.tdt == SD_F32 ? 4 : 2);
@@ -2422,28 +2418,10 @@ __device__ __forceinline__ uint32_t draw_tag(uint32_t epoch, int r, int c, int n
 // its normaliser is not finite (NaN / inf logits).
 constexpr float kGreedyDelta = 1.0f / 32.0f;
 
-// k_draw_lean A/B switches of the build.  SD_DRAW_PUB_CLAIM=1: the claiming wave publishes the
-// span's record itself, no second barrier (measured slower: 6.8 vs 6.5 us per bench draw, the
-// claiming wave is rarely wave 0).  SD_DRAW_POLL2=1: two staggered polls in flight (measured slower:
-// 7.2 vs 6.65 us per bench draw, 5.0 vs 4.5 at batch 1 — the row's last span is dispatched last and
-// usually finds every record at its first poll, so the stagger only delays it).
-#ifndef SD_DRAW_PUB_CLAIM
-#define SD_DRAW_PUB_CLAIM 0
-#endif
-#ifndef SD_DRAW_POLL2
-#define SD_DRAW_POLL2 0
-#endif
-#ifndef SD_DRAW_VALU_TRIM
-#define SD_DRAW_VALU_TRIM 1   // integer-key wave max, no per-element select (A/B: 0)
-#endif
-#if SD_DRAW_VALU_TRIM
-#define SD_DRAW_WMAX wave_max_ord   // the tail's maxima: finite or -inf records, never NaN
-#else
-#define SD_DRAW_WMAX wave_max
-#endif
-#ifndef SD_DRAW_STAGGER
-#define SD_DRAW_STAGGER 8   // the second poll's delay, in s_sleep units of 64 clocks
-#endif
+// Variants measured slower and parked as patches (scripts/experiments/draw_lean_variants.patch):
+// the claiming wave publishing the span's record itself (6.8 vs 6.5 us per bench draw), two
+// staggered polls in flight (7.2 vs 6.65 us), an fp64 CDF span pick instead of the Gumbel race, and
+// fmaxf wave maxima with a per-element -inf select (6.80 vs 6.50 us).
 
 template <int DT, int NST>
 __device__ int greedy_rescan(const DrawLean& A, const char* row, int c, float M, float S) {
@@ -2505,39 +2483,27 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     __shared__ int32_t l_j;
     __shared__ float l_y;
     __shared__ int32_t l_fi[NW], l_dirty[NW];
-    __shared__ uint32_t l_epoch;
     uint32_t epoch = 0;   // poll mode: this launch's epoch of row r (read by wave 0, beside the loads)
     if (w == 0) {   // the span's in-chunk uniform: one wave's scalar unit, while the loads fly
         if (A.poll) epoch = __hip_atomic_load(seq_counter(A.cnt, 2, r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const double u = GREEDY ? 0.0 : cdf_uniform(A.noise, (uint32_t)r, 1u + (uint32_t)c);
-        if (lane == 0) {
-            l_u = u; l_j = -1; l_y = -INFINITY;
-            if constexpr (!GREEDY && SD_DRAW_PUB_CLAIM) l_epoch = epoch;   // (waits for the epoch load)
-        }
+        if (lane == 0) { l_u = u; l_j = -1; l_y = -INFINITY; }
     }
     // per-wave max and weights: no barrier before the exps
     float mv = y[0];
 #pragma unroll
     for (int k = 1; k < EPT; ++k) mv = fmaxf(mv, y[k]);
-#if SD_DRAW_VALU_TRIM
     // integer-key wave max; a wave of -inf entries subtracts 0 (its weights are exp2(-inf) = 0),
     // so no per-element select, and a NaN entry always makes its own weight NaN (the span's S_c
     // NaN flags the row)
     const float mw = wave_max_ord(mv);
     const float mws = mw > -INFINITY ? mw : 0.f;
-#else
-    const float mw = wave_max(mv);
-#endif
     SD_TSL(ts_wg, 1);
     float wv[EPT];
     float tl = 0.f;
 #pragma unroll
     for (int k = 0; k < EPT; ++k) {
-#if SD_DRAW_VALU_TRIM
         wv[k] = __builtin_amdgcn_exp2f((y[k] - mws) * kLog2e);
-#else
-        wv[k] = mw > -INFINITY ? __builtin_amdgcn_exp2f((y[k] - mw) * kLog2e) : 0.f;
-#endif
         tl += wv[k];
     }
     const float incl = wave_incl_scan(tl);             // lane order, relative to mw
@@ -2550,14 +2516,12 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     for (int k = 1; k < NW; ++k) m = fmaxf(m, l_m[k]);
     float off = 0.f, my_off = 0.f, my_sc = 0.f, my_W = 0.f;
     int lastw = -1;
-    float l_off[NW], l_W[NW];   // (registers) every wave's offset and weight
 #pragma unroll
     for (int k = 0; k < NW; ++k) {
         const float sc = l_m[k] > -INFINITY ? __builtin_amdgcn_exp2f((l_m[k] - m) * kLog2e) : 0.f;
         const float Wk = l_s[k] * sc;
         if (k == w) { my_off = off; my_sc = sc; my_W = Wk; }
         if (Wk > 0.f) lastw = k;
-        l_off[k] = off; l_W[k] = Wk;
         off += Wk;
     }
     const float T = off;
@@ -2578,18 +2542,8 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     }
     const float t = (float)(l_u * (double)T);
     // the claiming wave (rounding past the end: the last wave with weight)
-    constexpr bool kPub = !GREEDY && SD_DRAW_PUB_CLAIM;
-    int cw = -1;   // kPub: every thread knows the claiming wave
-    if constexpr (kPub) {
-#pragma unroll
-        for (int k = 0; k < NW; ++k)
-            if (cw < 0 && l_W[k] > 0.f &&
-                ((t >= l_off[k] && t < l_off[k] + l_W[k]) || (k == lastw && t >= l_off[k] + l_W[k])))
-                cw = k;
-    }
-    const bool claim = !GREEDY && (kPub ? cw == w
-                                        : my_W > 0.f && ((t >= my_off && t < my_off + my_W) ||
-                                                         (w == lastw && t >= my_off + my_W)));
+    const bool claim = !GREEDY && my_W > 0.f && ((t >= my_off && t < my_off + my_W) ||
+                                                 (w == lastw && t >= my_off + my_W));
     int32_t cj = -1;   // the claiming lane's element and its logit
     float cy = -INFINITY;
     int hl = -1;
@@ -2619,25 +2573,14 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             }
         }
     }
-    if constexpr (kPub) {
-        // the claiming wave publishes and (last span) runs the tail: no second barrier; wave 0 when
-        // no wave claims (a span of zero or NaN weight)
-        if (w != (cw >= 0 ? cw : 0)) return;
-        if (hl >= 0) {
-            cj = __builtin_amdgcn_readlane(cj, hl);
-            cy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cy), hl));
-        }
-        epoch = l_epoch;
-    } else {
-        if (claim && lane == hl) { l_j = cj; l_y = cy; }
-        __syncthreads();
-        SD_TSL(ts_wg, 2);
-        if (w != 0) return;
-    }
+    if (claim && lane == hl) { l_j = cj; l_y = cy; }
+    __syncthreads();
+    SD_TSL(ts_wg, 2);
+    if (w != 0) return;
     const bool bad = T != T;   // NaN / +inf in the span: S_c NaN flags the row
     const float m_pub = bad && !(m > -INFINITY) ? 0.f : m, s_pub = bad ? NAN : T;
-    int32_t j_pub = kPub ? cj : l_j;
-    float y_pub = kPub ? cy : l_y;
+    int32_t j_pub = l_j;
+    float y_pub = l_y;
     int32_t g_dirty = 0;   // GREEDY: another value within kGreedyDelta of the span max
     if constexpr (GREEDY) {
         j_pub = l_fi[0];
@@ -2684,9 +2627,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     int32_t jk[2];
     bool dk[2] = {false, false};   // GREEDY: the span's dirty flag
     const int npass = (A.n_span + kWave - 1) / kWave;   // <= 2 (host: n_span <= 128)
-#ifdef SD_DRAW_CDF_PICK
-    const double u_row = GREEDY ? 0.0 : cdf_uniform(A.noise, (uint32_t)r);   // scalar unit, before the wait
-#else
     // the span race's Gumbel noise, one span per lane and pass, before the wait (off the chain)
     float gk[2] = {0.f, 0.f};
     if constexpr (!GREEDY) {
@@ -2696,7 +2636,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             if (q < npass && k < A.n_span) gk[q] = span_gumbel(A.noise, (uint32_t)r, (uint32_t)k);
         }
     }
-#endif
     if (A.poll) {
         // every other span's record, re-read until its tag is this launch's; this span's own from
         // registers (the lane that would hold it)
@@ -2708,45 +2647,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             have[q] = !(q < npass && k < A.n_span) || k == c;
             rec[q] = make_uint4(0u, 0u, 0u, 0u);
         }
-#if SD_DRAW_POLL2
-        // Two polls in flight, staggered: a record that lands just after one poll's read is seen by
-        // the other about half a round trip later instead of a whole one.  The tags are computed
-        // before the wait (off the chain); each poll's loads are waited on separately.
-        uint32_t tg[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) tg[q] = draw_tag(epoch, r, q * kWave + lane, A.n_span);
-        uint4 ra[2], rb[2];
-        const bool live = A.spin_limit >= 0;   // < 0: the test hook, every record counts as lost
-        if (live) {
-#pragma unroll
-            for (int q = 0; q < 2; ++q)
-                if (!have[q]) ra[q] = ld_coh16(pr + 2 * (q * kWave + lane));
-            __builtin_amdgcn_s_sleep(SD_DRAW_STAGGER);
-        }
-        for (int spin = 0;; ++spin) {
-            if (live) {
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    if (!have[q]) rb[q] = ld_coh16(pr + 2 * (q * kWave + lane));
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    if (!have[q] && ra[q].w == tg[q]) { have[q] = true; rec[q] = ra[q]; }
-                if (__all(have[0] && have[1])) break;
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    if (!have[q]) ra[q] = ld_coh16(pr + 2 * (q * kWave + lane));
-#pragma unroll
-                for (int q = 0; q < 2; ++q)
-                    if (!have[q] && rb[q].w == tg[q]) { have[q] = true; rec[q] = rb[q]; }
-                if (__all(have[0] && have[1])) break;
-            }
-            if (!spin_more(spin, A.spin_limit)) {   // bounded: ~tens of ms; the row is flagged, never a hang
-                xstat = SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#else
         for (int spin = 0;; ++spin) {
             if (A.spin_limit >= 0) {   // < 0: the test hook, every record counts as lost
 #pragma unroll
@@ -2764,7 +2664,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             }
             __builtin_amdgcn_s_sleep(1);
         }
-#endif
         SD_TSL(ts_wg, 4);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
@@ -2795,7 +2694,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         M = fmaxf(M, mk[q]);
     }
     }
-    M = SD_DRAW_WMAX(M);
+    M = wave_max_ord(M);   // the tail's maxima: finite or -inf records, never NaN
     float wk[2], S = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
@@ -2850,7 +2749,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         }
         return;
     }
-#ifndef SD_DRAW_CDF_PICK
     // span pick by a Gumbel race: argmax_c (m_c + ln S_c + g_c) picks span c with probability
     // S_c e^(m_c) / Σ — independent of M and S, so its wave max runs beside theirs (no fp64 scan)
     float key[2];
@@ -2860,7 +2758,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         key[q] = mk[q] > -INFINITY && sk[q] > 0.f ? mk[q] + __logf(sk[q]) + gk[q] : -INFINITY;
         kmax = fmaxf(kmax, key[q]);
     }
-    kmax = SD_DRAW_WMAX(kmax);
+    kmax = wave_max_ord(kmax);
     int pick = -1;
     if (kmax > -INFINITY) {
 #pragma unroll
@@ -2869,29 +2767,6 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             if (pick < 0 && hit) pick = q * kWave + __builtin_ctzll(hit);
         }
     }
-#else
-    // span pick: first span whose fp64 running total (span order) exceeds u * Σ.  One fp64 scan
-    // per pass (reused for the total), and only the passes the row has (one for V <= 128 Ki)
-    double sincl[2] = {0.0, 0.0};
-    double tot = 0.0;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        if (q < npass) {
-            sincl[q] = tot + wave_incl_scan_d((double)wk[q]);
-            tot = lane_d(sincl[q], 63);
-        }
-    }
-    const double tt = u_row * tot;
-    int pick = -1, lastpos = -1;
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        if (q >= npass) break;
-        const uint64_t hit = __ballot(sincl[q] > tt && wk[q] > 0.f), posm = __ballot(wk[q] > 0.f);
-        if (pick < 0 && hit) pick = q * kWave + __builtin_ctzll(hit);
-        if (posm) lastpos = q * kWave + 63 - __builtin_clzll(posm);
-    }
-    if (pick < 0) pick = lastpos;   // rounding left t at / after the total: the last positive span
-#endif
     int32_t x = -1;
     float yx = -INFINITY;
     if (pick >= 0) {
@@ -3339,6 +3214,10 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
         }
         cap = it->second;
     }
+    // headroom: every workgroup polls its sequence's others, so the whole grid must be resident; a
+    // kernel of another stream holding some CUs must not push it past that, so the grid takes at
+    // most half the device's slots (at V = 128256: up to 4 sequences); beyond, k_stats + k_sample
+    if (2 * (int64_t)P0.B * n_span > cap && mode < 0) { lean_why(11); return 0; }
     if ((int64_t)P0.B * n_span > cap) { lean_why(11); return 0; }
     sd::Plan P = P0;
     P.n_chunks = n_span;

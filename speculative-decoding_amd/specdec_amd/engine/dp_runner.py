@@ -1,31 +1,39 @@
-"""Data-parallel runner for the drop-in engine: one process per GPU, the prompt batch split by row.
+"""Data-parallel runners for the drop-in engine: one process per GPU, no collective on the data path.
 
-The reference runs each prompt batch of engine/benchmark_executor.py:72-83 on one device
-(``infer_batch(runner, prompts)``).  Prompt rows are independent, so here every rank of a
-``torch.distributed`` job (one process per GPU; RCCL or gloo — only host objects are exchanged,
-after decoding) takes a contiguous row shard of the SAME tokenized global batch (the padding
-depends on the whole batch, so the batch is tokenized once, identically on every rank), runs
-``batch_speculative_generate`` on it with ``ctx.row_base`` = its first global row, and the
-per-row outputs / rates / request metrics are gathered in global row order.
+Two ways to split the work (INTEGRATION.md "Data parallelism" says which is exact):
 
-Noise: data parallelism is PHILOX-only.  Philox draws are keyed by (seed, call offset, GLOBAL row),
-so the gathered outputs equal those of one process decoding the whole batch
-(tests/test_gpu_engine_surface.py); after every batch the ranks agree on the call offset (the
-largest any rank reached — what one process, which runs until its last row finishes, would hold),
-so later batches stay equal too.  The bit-exact STREAM mode draws from ONE torch generator in the
-reference's serial row order (engine/infer_engine.py:280-330): independent ranks would each replay
-the same words, so ``batch_speculative_generate_dp`` refuses it (RuntimeError) rather than return
-outputs that match neither the reference nor one process.
+* **Batch-level (bit-exact in both noise modes)** — ``infer_batches_dp`` / ``generate_batches_dp``.
+  The reference's benchmark loop re-seeds before EVERY prompt batch (engine/benchmark_executor.py:79,
+  ``runner._set_seed(42)`` -> engine/benchmark_runner.py:164-172) and runs each batch on its own
+  (:72-83).  A batch's outputs therefore depend only on its prompts and the seed, so the batches can
+  be dealt to the ranks round-robin (batch i on rank i % world), each rank re-seeding before each of
+  its batches exactly as the reference does, and every batch's tokens equal one process's — also under
+  the STREAM noise (the reference's own torch-generator draws).  Results are gathered in batch order
+  with ``all_gather_object`` after decoding.
 
-There is no collective on the data path: the exchanges are ``all_gather_object`` of the finished
-rows' host results and of the call offsets.  Ranks that share a GPU (more ranks than devices on a
-node) make the library's in-launch polls unsafe (a grid can be starved by another process's
-kernels), so the runner switches them off (``sd_set_poll_policy(allow_poll=0)``) when it sees that.
+* **Row-level (Philox only; strong scaling of ONE batch)** — ``batch_speculative_generate_dp`` /
+  ``run_batch_speculative_dp`` / ``infer_batch_dp``.  Every rank takes a contiguous row shard of the
+  SAME tokenized global batch (the padding depends on the whole batch, so the batch is tokenized
+  once, identically on every rank), runs ``batch_speculative_generate`` on it with ``ctx.row_base`` =
+  its first global row, and the per-row outputs / rates / request metrics are gathered in global
+  row order.  Philox draws are keyed by (seed, call offset, GLOBAL row), so the gathered outputs
+  equal those of one process decoding the whole batch (tests/test_gpu_engine_surface.py); after
+  every batch the ranks agree on the call offset (the largest any rank reached — what one process,
+  which runs until its last row finishes, would hold), so later batches stay equal too.  The
+  bit-exact STREAM mode draws from ONE torch generator in the reference's serial row order
+  (engine/infer_engine.py:280-330): independent ranks would each replay the same words, so the
+  row-level runner refuses it (RuntimeError) rather than return outputs that match neither the
+  reference nor one process.
+
+Ranks that share a GPU (more ranks than devices on a node) make the library's in-launch polls
+unsafe (a grid can be starved by another process's kernels), so both runners switch them off
+(``sd_set_poll_policy(allow_poll=0)``) when they see that.
 """
 from __future__ import annotations
 
+import random
 import time
-from typing import List, Optional, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 
@@ -108,7 +116,16 @@ def batch_speculative_generate_dp(ctx, input_ids: torch.Tensor, attention_mask: 
     start, stop = dp.shard_rows(B, world, rank)
     saved = getattr(ctx, "row_base", None)
     ctx.row_base = start
-    cb = None if first_token_callback is None else (lambda i: first_token_callback(start + i))
+    cb = None
+    if first_token_callback is not None:
+        takes_time = getattr(first_token_callback, "accepts_time", False)
+
+        def cb(i, t=None):   # local row -> global row; the graph path's device time is forwarded
+            if takes_time:
+                first_token_callback(start + i, t)
+            else:
+                first_token_callback(start + i)
+        cb.accepts_time = takes_time
     err = None
     outs, rates = [], []
     t0 = time.time()
@@ -142,9 +159,10 @@ def run_batch_speculative_dp(ctx, input_ids: torch.Tensor, attention_mask: torch
     bm = BatchMetrics(batch_size=batch_size)
     firsts: List[Optional[float]] = [None] * batch_size
 
-    def first_token(idx):
+    def first_token(idx, t=None):
         if idx < batch_size and firsts[idx] is None:
-            firsts[idx] = time.time()
+            firsts[idx] = time.time() if t is None else t
+    first_token.accepts_time = True   # the graph path reports the first draw's device completion time
 
     ok = True
     t_start = time.time()
@@ -190,3 +208,90 @@ def infer_batch_dp(ctx, prompts: List[str], dist=None) -> Tuple[Optional[BatchMe
     if getattr(ctx, "reset_in_between", False) and getattr(ctx, "ngram", None) is not None:
         ctx.ngram.reset()
     return run_batch_speculative_dp(ctx, input_ids, attention_mask, len(prompts), dist), None
+
+
+# ---------------------------------------------------------------------------------------------
+# batch-level data parallelism (bit-exact under STREAM and Philox)
+# ---------------------------------------------------------------------------------------------
+
+def reseed(seed: int) -> None:
+    """engine/benchmark_runner.py:164-172 (``_set_seed``), run before every batch by
+    engine/benchmark_executor.py:79: python, numpy and torch generators seeded.  The STREAM noise
+    draws from torch.default_generator, so this fixes its words; a Philox default noise restarts
+    its call counter (its seed is fixed by ``set_noise_mode``), the Philox analogue."""
+    random.seed(seed)
+    try:
+        import numpy as np
+        np.random.seed(seed)
+    except ImportError:   # pragma: no cover - numpy is part of the image
+        pass
+    torch.manual_seed(seed)
+    noise = default_noise()
+    if isinstance(noise, PhiloxNoise):
+        noise.offset = 0
+
+
+def batches_of_rank(n_batches: int, world: int, rank: int) -> List[int]:
+    """The batches rank `rank` decodes: i % world == rank (round-robin, so ranks stay balanced when
+    the batch count is not a multiple of the world size)."""
+    if world <= 0 or not 0 <= rank < world or n_batches < 0:
+        raise ValueError(f"bad batch assignment: batches={n_batches} world={world} rank={rank}")
+    return list(range(rank, n_batches, world))
+
+
+def _gather_in_order(mine, n_batches: int, dist, what: str):
+    """[(batch index, result or error text)] of every rank -> results in batch order; raises on
+    every rank if any rank failed (after the gather, so no rank is left waiting in it)."""
+    got = {}
+    errs = []
+    for part in _gather(mine, dist):
+        for i, ok, res in part:
+            if ok:
+                got[i] = res
+            else:
+                errs.append(res)
+    if errs:
+        raise RuntimeError(f"{what}: " + "; ".join(errs))
+    return [got[i] for i in range(n_batches)]
+
+
+def generate_batches_dp(ctx, batches: Sequence[Tuple[torch.Tensor, torch.Tensor]], dist=None, seed: int = 42):
+    """Decode whole prompt batches ``[(input_ids [B_i, L_i], attention_mask)]`` dealt round-robin
+    over the ranks, re-seeding before each batch (``reseed(seed)``) as the reference's benchmark
+    loop does.  Returns, on every rank, ``[(outputs, rates)]`` in batch order (outputs on the CPU)
+    and this rank's decode wall time.  Bit-exact in both noise modes: every batch equals what one
+    process running the same re-seeded loop returns."""
+    world, rank = _world(dist)
+    if batches:
+        configure_residency(dist, batches[0][0].device)
+    mine = []
+    t0 = time.time()
+    for i in batches_of_rank(len(batches), world, rank):
+        ids, mask = batches[i]
+        reseed(seed)
+        try:
+            outs, rates = batch_speculative_generate(ctx, ids, mask, ids.shape[0])
+            mine.append((i, True, ([o.cpu() for o in outs], rates)))
+        except Exception as e:   # reported after the gather
+            mine.append((i, False, f"rank {rank} batch {i}: {type(e).__name__}: {e}"))
+    elapsed = time.time() - t0
+    return _gather_in_order(mine, len(batches), dist, "generate_batches_dp"), elapsed
+
+
+def infer_batches_dp(ctx, prompt_batches: Sequence[List[str]], dist=None, seed: int = 42
+                     ) -> List[Tuple[Optional[BatchMetrics], Optional[BatchMetrics]]]:
+    """engine/benchmark_executor.py:72-83's batch loop, sharded by batch: rank r runs
+    ``reseed(seed); infer_batch(ctx, prompts)`` for batches r, r + world, ...; every rank returns
+    the ``(spec_metrics, target_metrics)`` pair of EVERY batch, in batch order (what the reference
+    appends to its BenchmarkResults).  A failed batch is ``(None, None)``, as infer_batch returns it
+    (:144-146)."""
+    from .infer_engine import infer_batch
+    world, rank = _world(dist)
+    dev = getattr(ctx, "drafter_device", None) or getattr(ctx, "target_device", None)
+    if dev is not None:
+        configure_residency(dist, dev)
+    mine = []
+    for i in batches_of_rank(len(prompt_batches), world, rank):
+        reseed(seed)
+        mine.append((i, True, infer_batch(ctx, list(prompt_batches[i]))))
+    return _gather_in_order(mine, len(prompt_batches), dist, "infer_batches_dp")

@@ -92,7 +92,7 @@ class EngineWindow:
             logits = self.drafter_step(prev, d, self.step_dev)
             samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, self.noise, row_base=self.row_base,
                                         row_stats_out=self.dstats[d], status_or=self.err)
-            samples.clamp_(min=0)                        # a failed row's -1 never reaches a forward
+            samples.clamp_(0, logits.shape[-1] - 1)      # a failed row's -1 never reaches a forward
             if d == 0 and self.first_draw_event is not None and not self._first_recorded \
                     and not torch.cuda.is_current_stream_capturing():
                 self.first_draw_event.record()           # TTFT: the first draft of the first window

@@ -225,7 +225,7 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
         finally:
             noise.offset = win.o0 + win.windows_run * (gamma + 1)         # the calls the windows consumed
         outs = _collect(input_ids, win.generated, win.drafted, win.accepted, B, win.err)
-        if first_token_callback is not None:
+        if first_token_callback is not None and win._first_recorded:     # gen_len 0: no first token
             t_first = t_ref + ref.elapsed_time(win.first_draw_event) / 1e3
             for idx in range(B):                                          # step 0: every row is active
                 if getattr(first_token_callback, "accepts_time", False):
@@ -273,7 +273,7 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
             samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise,     # :241-246 softmax + multinomial
                                         row_base=row_base, row_stats_out=dstats[d] if stash else None,
                                         status_or=err)
-            samples.clamp_(min=0)   # a failed row's -1 (raised at the next read of err) never reaches a forward
+            samples.clamp_(0, logits.shape[-1] - 1)   # a failed row's -1 (raised at the next read of err) never reaches a forward
             rows.append(logits)
             draft_tokens[:, d] = torch.where(active, samples, draft_tokens[:, d])          # :252
             generated[:, step + d] = torch.where(active, samples, generated[:, step + d])  # :257

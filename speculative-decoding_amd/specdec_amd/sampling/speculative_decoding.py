@@ -158,7 +158,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
                 noise.reserve(g * 2 * V + g + 2 * V, dev)
             tok = ids_d[0, cur + k:cur + k + 1]
             sample_rows(row, spec, noise, tokens_out=tok, row_stats_out=dstats[k] if stash else None, status_or=err_d)
-            tok.clamp_(min=0)
+            tok.clamp_(0, row.shape[-1] - 1)   # a failed row's -1 never reaches a forward
             draft_rows.append(row if row.device == torch.device(dev) else row.to(dev))
         drafts_speculated += g
         input_ids = ids_d.to(dev)

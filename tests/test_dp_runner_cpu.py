@@ -130,3 +130,125 @@ def test_dp_runner_orchestration_on_two_gloo_ranks():
         assert rec["ttft_set"]
         assert "row 5" in rec["fail"] and "rank 1" in rec["fail"]
         assert rec["fail_bm"] is None
+
+
+# ---------------------------------------------------------------------------------------------
+# batch-level data parallelism: whole batches per rank, re-seeded per batch (bit-exact, STREAM)
+# ---------------------------------------------------------------------------------------------
+
+def stream_engine(ctx, input_ids, attention_mask, batch_size, first_token_callback=None):
+    """Stand-in for batch_speculative_generate under the STREAM noise: every token comes from
+    torch.default_generator in the serial order one process consumes it (the reference's draws),
+    and the number of draws depends on the outcomes — so a batch's outputs depend on the generator
+    state it starts from, which only the per-batch re-seed makes rank-independent."""
+    outs, rates = [], []
+    for i in range(batch_size):
+        n = 1 + int(torch.randint(0, 4, (1,)))
+        gen = torch.randint(3, 1000, (n,))
+        outs.append(torch.cat([input_ids[i], gen]))
+        rates.append(float(torch.rand(1)))
+    return outs, rates
+
+
+def stream_batches(n):
+    g = torch.Generator().manual_seed(77)
+    return [torch.randint(3, 500, (2 + k % 3, 4), generator=g) for k in range(n)]
+
+
+def one_process_batches(batches, seed):
+    from specdec_amd.engine import dp_runner
+    res = []
+    for ids in batches:
+        dp_runner.reseed(seed)
+        outs, rates = stream_engine(None, ids, torch.ones_like(ids), ids.shape[0])
+        res.append(([o.tolist() for o in outs], rates))
+    return res
+
+
+def _batch_worker(rank, world, port, n_batches, seed, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from specdec_amd import set_noise_mode
+        from specdec_amd.engine import dp_runner, infer_engine
+        dp_runner.batch_speculative_generate = stream_engine
+        set_noise_mode("stream")
+        batches = [(ids, torch.ones_like(ids)) for ids in stream_batches(n_batches)]
+        torch.manual_seed(rank + 1000)        # the ranks' generators start apart: only reseed aligns them
+        res, _ = dp_runner.generate_batches_dp(SimpleNamespace(), batches, dist, seed=seed)
+        rec = {"batches": [([o.tolist() for o in outs], rates) for outs, rates in res],
+               "mine": dp_runner.batches_of_rank(n_batches, world, rank)}
+
+        # infer_batches_dp: the executor loop's (spec, target) pairs in batch order
+        def fake_infer(ctx, prompts):
+            return (len(prompts), float(torch.rand(1))), None
+        infer_engine.infer_batch = fake_infer
+        pairs = dp_runner.infer_batches_dp(SimpleNamespace(), [["p"] * (k + 1) for k in range(n_batches)], dist,
+                                           seed=seed)
+        rec["pairs"] = pairs
+        # a failing batch raises on every rank
+        def bad_engine(ctx, input_ids, attention_mask, batch_size, first_token_callback=None):
+            if int(input_ids[0, 0]) == int(batches[1][0][0, 0]):
+                raise RuntimeError("probability tensor contains either `inf`, `nan` or element < 0")
+            return stream_engine(ctx, input_ids, attention_mask, batch_size)
+        dp_runner.batch_speculative_generate = bad_engine
+        try:
+            dp_runner.generate_batches_dp(SimpleNamespace(), batches, dist, seed=seed)
+            rec["fail"] = "no error"
+        except RuntimeError as e:
+            rec["fail"] = str(e)
+        out.put((rank, rec))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_batch_level_dp_is_bit_exact_under_stream_noise():
+    """4 and 5 batches over 2 gloo ranks (round-robin) equal one process's re-seeded batch loop,
+    batch for batch, under the STREAM noise (engine/benchmark_executor.py:79 re-seeds per batch)."""
+    from specdec_amd import set_noise_mode
+    from specdec_amd.engine import dp_runner
+    seed, world = 42, 2
+    set_noise_mode("stream")
+    assert dp_runner.batches_of_rank(5, 2, 0) == [0, 2, 4] and dp_runner.batches_of_rank(5, 2, 1) == [1, 3]
+    for n_batches in (4, 5):
+        want = one_process_batches(stream_batches(n_batches), seed)
+        want_pairs = []
+        for k in range(n_batches):
+            dp_runner.reseed(seed)
+            want_pairs.append(((k + 1, float(torch.rand(1))), None))
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_batch_worker, args=(r, world, port, n_batches, seed, q)) for r in range(world)]
+        for p in procs:
+            p.start()
+        recs = dict(q.get(timeout=180) for _ in range(world))
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+        assert sorted(recs[0]["mine"] + recs[1]["mine"]) == list(range(n_batches))
+        for rank, rec in recs.items():
+            assert rec["batches"] == want, (n_batches, rank)
+            assert [tuple(p[0]) for p in rec["pairs"]] == [p[0] for p in want_pairs]
+            assert "batch 1" in rec["fail"] and "rank 1" in rec["fail"]
+
+
+def test_dp_runner_forwards_the_graph_paths_first_token_time(monkeypatch):
+    """The graph-window engine path reports each row's first draw at its device completion time
+    (callback(idx, t) when the callback declares accepts_time); the DP wrappers must forward it,
+    not stamp the time the whole run returned (TTFT ~ batch latency otherwise)."""
+    from specdec_amd import set_noise_mode
+    from specdec_amd.engine import dp_runner
+
+    def timed_engine(ctx, input_ids, attention_mask, batch_size, first_token_callback=None):
+        assert getattr(first_token_callback, "accepts_time", False)
+        for i in range(batch_size):
+            first_token_callback(i, 1000.0 + ctx.row_base + i)
+        return [torch.cat([input_ids[i], torch.tensor([5])]) for i in range(batch_size)], [0.5] * batch_size
+
+    monkeypatch.setattr(dp_runner, "batch_speculative_generate", timed_engine)
+    set_noise_mode("philox", seed=3)
+    ids = torch.arange(12, dtype=torch.long).reshape(4, 3) + 10
+    bm = dp_runner.run_batch_speculative_dp(SimpleNamespace(gamma=4), ids, torch.ones_like(ids), 4, None)
+    assert [r.first_token_time for r in bm.requests] == [1000.0, 1001.0, 1002.0, 1003.0]
+    set_noise_mode("stream")

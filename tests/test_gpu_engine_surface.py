@@ -126,3 +126,60 @@ def test_dp_runner_two_ranks_equal_one_process():
     assert polled is False          # both ranks on cuda:0: the runner switched in-launch polls off
     assert [g for g, _ in reqs] == [len(o) - ids.shape[1] for o in want]
     assert [a for _, a in reqs] == wrates
+
+
+def _batches_setup(V=4096):
+    target, drafter = make_pair(V, dtype=torch.bfloat16, device=DEV, pos_mult=0)
+    g = torch.Generator().manual_seed(5151)
+    batches = []
+    for k in range(4):
+        ids = torch.randint(3, V, (3 + k % 2, 6 + k), generator=g).to(DEV)
+        batches.append((ids, torch.ones_like(ids)))
+    ctx = SimpleNamespace(drafter=drafter, target=target, gamma=4, gen_len=16, end_tokens=[1])
+    return ctx, batches
+
+
+def _batch_dp_worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from specdec_amd import set_noise_mode
+        from specdec_amd.engine.dp_runner import generate_batches_dp
+        ctx, batches = _batches_setup()
+        set_noise_mode("stream")
+        torch.manual_seed(100 + rank)            # only the per-batch re-seed may align the ranks
+        res, _ = generate_batches_dp(ctx, batches, dist, seed=42)
+        if rank == 0:
+            out.put([([o.tolist() for o in outs], rates) for outs, rates in res])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_batch_level_dp_two_ranks_bit_exact_under_stream():
+    """Batch-level data parallelism on the real kernels: 4 prompt batches dealt over two processes
+    (both on cuda:0), each re-seeded per batch as engine/benchmark_executor.py:79 does, under the
+    bit-exact STREAM noise, equal one process's re-seeded loop batch for batch."""
+    from specdec_amd import set_noise_mode
+    from specdec_amd.engine.dp_runner import reseed
+    from specdec_amd.engine.infer_engine import batch_speculative_generate
+    ctx, batches = _batches_setup()
+    set_noise_mode("stream")
+    want = []
+    for ids, mask in batches:
+        reseed(42)
+        outs, rates = batch_speculative_generate(ctx, ids, mask, ids.shape[0])
+        want.append(([o.cpu().tolist() for o in outs], rates))
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_batch_dp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert got == want
+    assert any(len(o) > batches[i][0].shape[1] for i, (outs, _) in enumerate(want) for o in outs)

@@ -114,15 +114,19 @@ def test_speculative_generate_raises_like_torch(mode, where):
     torch.cuda.synchronize()
 
 
-def test_ngram_loop_raises_like_torch():
+@pytest.mark.parametrize("kind", ["multinomial", "nucleus"])
+def test_ngram_loop_raises_like_torch(kind):
+    """A NaN column in the target bank (under a nucleus processor: masked by the cut in most rows,
+    but torch's processed row is NaN all the same)."""
     from specdec_amd import RowError, set_noise_mode
     from specdec_amd.ngram_assisted import NGramStorage, ngram_assisted_speculative_generate
-    from specdec_amd.utils.logits_processor import MultinomialProcessor
+    from specdec_amd.utils.logits_processor import MultinomialProcessor, NucleusProcessor
     target, _ = nan_pair(where="target")
+    proc = MultinomialProcessor(1.0) if kind == "multinomial" else NucleusProcessor(1.0, 0.9)
     set_noise_mode("stream")
     with pytest.raises(RowError, match="nan"):
         ngram_assisted_speculative_generate([5, 9, 13, 5, 9], NGramStorage(n=3, vocab_size=4096), target, gamma=4,
-                                            logits_processor=MultinomialProcessor(1.0), max_gen_len=10)
+                                            logits_processor=proc, max_gen_len=10)
 
 
 @pytest.mark.parametrize("graph", [False, True])
@@ -224,8 +228,8 @@ def test_nan_block_flags_like_a_nan_row(block):
     dl = (tl[:, :g].float() + torch.randn(1, g, V, generator=gen)).to(torch.bfloat16)
     tl, dl = tl.to(DEV), dl.to(DEV)
     off, n = block
-    # (plain rows in both noise modes; nucleus rows through the Philox rejection draw. A NaN that a
-    # top-k / nucleus keep masks out on the threshold path is not flagged yet: DESIGN.md §8.)
+    # (plain rows in both noise modes; nucleus rows through the Philox rejection draw; the masked
+    # NaN under a top-k / nucleus keep: test_nan_under_keep_is_a_nan_row below)
     cases = [(ops.PLAIN_SOFTMAX, PhiloxNoise(seed=3)), (ops.PLAIN_SOFTMAX, StreamNoise(torch.Generator().manual_seed(3))),
              (ops.ProcSpec("nucleus", 1.0, 0, 0.9), PhiloxNoise(seed=3))]
     for spec, noise in cases:
@@ -256,3 +260,100 @@ def test_nan_block_flags_like_a_nan_row(block):
         mask = _lib.SD_ROW_ERROR_MASK
         assert int(a.row_status[0]) & mask == int(b.row_status[0]) & mask, (slot, int(a.row_status[0]), int(b.row_status[0]))
         assert int(a.n_accepted[0]) == int(b.n_accepted[0]), slot
+
+
+@pytest.mark.parametrize("fill", ["nan", "-inf"])
+def test_stream_race_invalid_row_token_is_minus_one(fill):
+    """The STREAM three-launch draw (T != 1 takes it): an all-NaN or all -inf row has no race
+    candidate at all.  torch.multinomial raises on it; here the row is flagged invalid and its token
+    is -1 (never an index past the vocabulary that a clamp(min=0) would let into a forward)."""
+    from specdec_amd import StreamNoise, _lib, ops
+    x = (torch.randn(3, 4096, device=DEV) * 3).to(torch.bfloat16)
+    x[1] = float(fill)
+    tok, _, st = ops.sample_rows(x, ops.ProcSpec("multinomial", 0.7), StreamNoise(torch.Generator().manual_seed(2)))
+    tok, st = tok.cpu(), st.cpu()
+    assert int(tok[1]) == -1 and st[1] & _lib.SD_ROW_INVALID_DIST
+    assert all(0 <= int(tok[r]) < 4096 for r in (0, 2))
+    assert not (st[torch.tensor([0, 2])] & _lib.SD_ROW_ERROR_MASK).any()
+
+
+KEEP_PROCS = [("topk", 1.0, 50, 0.0), ("nucleus", 1.0, 0, 0.9), ("topknucleus", 1.0, 50, 0.9), ("topk", 0.7, 50, 0.0),
+              ("nucleus", 0.7, 0, 0.9)]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("fill", ["nan", "inf"])
+def test_nan_under_keep_is_a_nan_row(dtype, fill):
+    """A NaN or +inf logit that the top-k / nucleus cut would mask out: torch's topk / sort rank it
+    first (NaN) or keep it (+inf, whose softmax is NaN), so the reference's processed row is NaN
+    throughout and torch.multinomial raises on it (utils/logits_processor.py:59-63,73-81; checked on
+    the oracle below).  The HIP path: sd_probs returns an all-NaN row, every draw of it — both noise
+    modes, the threshold path and the Philox rejection draw — is SD_ROW_INVALID_DIST with token -1,
+    and the verify treats such a target row exactly as a NaN row; the clean row beside it is
+    untouched."""
+    from specdec_amd import PhiloxNoise, StreamNoise, _lib, ops
+    V, g = 128256, 4
+    gen = torch.Generator().manual_seed(31)
+    x = (torch.randn(2, V, generator=gen) * 3).to(dtype)
+    lo = int(x[0].float().argmin())                  # far below any cut: masked by every processor
+    x[0, lo] = float(fill)
+    for kind, T, k, p in KEEP_PROCS:
+        proc = ref.Processor(kind, T, k, p)
+        want = ref.process(x[:1], proc)
+        assert want.isnan().all(), kind                  # the reference's processed row is NaN
+        spec = ops.ProcSpec(kind, T, k, p)
+        got = ops.probs_rows(x.to(DEV), spec).float().cpu()
+        assert got[0].isnan().all(), (kind, T)
+        assert not got[1].isnan().any(), (kind, T)
+        for noise in (PhiloxNoise(seed=5), StreamNoise(torch.Generator().manual_seed(5))):
+            tok, _, st = ops.sample_rows(x.to(DEV), spec, noise)
+            tok, st = tok.cpu(), st.cpu()
+            what = (kind, T, type(noise).__name__, int(st[0]), int(tok[0]))
+            assert st[0] & _lib.SD_ROW_INVALID_DIST and int(tok[0]) == -1, what
+            assert not st[1] & _lib.SD_ROW_ERROR_MASK and 0 <= int(tok[1]) < V, what
+
+    # the verify: a target row with the masked NaN / inf equals a NaN row (status and accept count)
+    if dtype != torch.bfloat16:
+        return
+    tl = (torch.randn(1, g + 1, V, generator=gen) * 3).to(dtype)
+    dl = (tl[:, :g].float() + torch.randn(1, g, V, generator=gen)).to(dtype)
+    tl, dl = tl.to(DEV), dl.to(DEV)
+    for kind, T, k, p in KEEP_PROCS[:3]:
+        spec = ops.ProcSpec(kind, T, k, p)
+        for mode in ("philox", "stream"):
+            def run(trows):
+                noise = PhiloxNoise(seed=9) if mode == "philox" else StreamNoise(torch.Generator().manual_seed(9))
+                ids = torch.empty(1, g, dtype=torch.long, device=DEV)
+                for d in range(g):
+                    tok, _, _ = ops.sample_rows(dl[:, d], spec, noise)
+                    ids[:, d] = tok
+                return ops.verify([trows[:, t] for t in range(g + 1)], [dl[:, d] for d in range(g)], ids,
+                                  _lib.SD_RULE_SPEC, spec, spec, noise)
+            for slot in (0, g):
+                tb, tw = tl.clone(), tl.clone()
+                tb[0, slot, int(tl[0, slot].float().argmin())] = float(fill)
+                tw[0, slot, :] = float("nan")
+                a, b = run(tb), run(tw)
+                mask = _lib.SD_ROW_ERROR_MASK
+                assert int(a.row_status[0]) & mask == int(b.row_status[0]) & mask, (kind, mode, slot)
+                assert int(a.n_accepted[0]) == int(b.n_accepted[0]), (kind, mode, slot)
+
+
+@pytest.mark.parametrize("mode", ["stream", "philox"])
+@pytest.mark.parametrize("kind", ["topk", "nucleus"])
+def test_speculative_generate_raises_on_masked_nan(mode, kind):
+    """The drop-in loop under a top-k / nucleus processor with one NaN logit per row (column 0,
+    masked by the cut in almost every bank row): the reference raises in torch.multinomial, and so
+    does speculative_generate (RowError, a RuntimeError)."""
+    from specdec_amd import RowError, set_noise_mode
+    from specdec_amd.sampling import speculative_generate
+    from specdec_amd.utils.logits_processor import NucleusProcessor, TopKProcessor
+    target, drafter = nan_pair(where="drafter")
+    proc = TopKProcessor(1.0, 20) if kind == "topk" else NucleusProcessor(1.0, 0.9)
+    set_noise_mode(mode, seed=3)
+    try:
+        with pytest.raises(RowError, match="nan"):
+            speculative_generate([5, 9, 13], drafter, target, gamma=4, logits_processor=proc, max_gen_len=12)
+    finally:
+        set_noise_mode("stream")
+    torch.cuda.synchronize()
