@@ -65,6 +65,9 @@ def parse():
     ap.add_argument("--stream-steps", type=int, default=5, help="STREAM-mode (bit-exact noise) steps; 0 = skip")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] / configs[4] batch-1 lines")
     ap.add_argument("--no-shards", action="store_true", help="skip the 16 / 8 / 4-row shard lines")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end line (random-init Llama-3-8B / 3.2-1B shaped models, drop-in engine)")
+    ap.add_argument("--e2e-gen", type=int, default=64, help="new tokens per row in the end-to-end line")
     ap.add_argument("--trials", type=int, default=5,
                     help="timed trials of exactly --steps steps each (median reported)")
     ap.add_argument("--profile-only", action="store_true",
@@ -74,7 +77,7 @@ def parse():
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsing N ranks on fewer GPUs)")
     a = ap.parse_args()
     if a.profile_only:
-        a.no_cpu_baseline = a.no_configs1 = a.no_shards = True
+        a.no_cpu_baseline = a.no_configs1 = a.no_shards = a.no_e2e = True
         a.stream_steps = 0
     return a
 
@@ -350,6 +353,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_configs1:
         cfg1 = configs1_lines(dev, args, ops, _lib, PhiloxNoise)
         cfg4 = configs4_line(dev, args, ops, _lib, PhiloxNoise)
+    e2e = None
+    if rank == 0 and world == 1 and not args.no_e2e:
+        e2e = e2e_line(args)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(tl, dl, step.draft, args)
@@ -412,6 +418,7 @@ def main():
             "shard_rows": shards,
             "configs1": cfg1,
             "configs4": cfg4,
+            "e2e": e2e,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -541,6 +548,21 @@ def configs1_lines(dev, args, ops, _lib, PhiloxNoise):
         res[name] = {"us_per_step": dt / (len(outs) * replays) * 1e6, "tokens_per_s": tokens / dt,
                      "alg_bytes_per_step": (2 * g + 1) * V * 2}
     return res
+
+
+def e2e_line(args):
+    """The whole loop end to end (engine/infer_engine.py:99-146, the metric's own definition:
+    engine/metrics.py:100-105 output tokens / wall time): random-init Llama-3-8B / Llama-3.2-1B shaped
+    transformers models (bf16, no checkpoint exists offline) driving the drop-in
+    batch_speculative_generate at B = 32, γ = 4 in both noise modes, with the hot path's device time
+    (HIP events around every sd_sample / sd_verify call) against the wall time.  Random weights make
+    the acceptance rate meaningless; tokens/s and the hot path's share are the measurement."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import e2e_timing
+    try:
+        return e2e_timing.run(batch=args.batch, gen=args.e2e_gen, gamma=args.gamma)
+    except Exception as e:   # reported, never fatal to the headline line
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def cpu_model_name():

@@ -35,8 +35,8 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 8
-#define SD_MAX_GAMMA 16
+#define SD_ABI_VERSION 9
+#define SD_MAX_GAMMA 32
 
 typedef enum {
     SD_OK = 0,

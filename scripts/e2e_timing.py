@@ -71,6 +71,59 @@ class HotPathTimer:
             setattr(mod, name, fn)
 
 
+def run(batch=32, prompt=128, gen=64, gamma=4, layers_8b=32, layers_1b=16, modes=("philox", "stream")):
+    """Build the two random-init models, run the drop-in engine once per noise mode (after a warm-up
+    run) and return the report dict."""
+    from specdec_amd import set_noise_mode
+    from specdec_amd.engine import infer_engine
+    t0 = time.time()
+    target = llama(4096, 14336, layers_8b, 32, 8)      # Llama-3-8B shape
+    drafter = llama(2048, 8192, layers_1b, 32, 8)      # Llama-3.2-1B shape
+    torch.cuda.synchronize()
+    build_s = time.time() - t0
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(1000, 120000, (batch, prompt), generator=g).cuda()
+    mask = torch.ones_like(ids)
+    from types import SimpleNamespace
+    ctx = SimpleNamespace(drafter=drafter, target=target, gamma=gamma, gen_len=gen,
+                          end_tokens=[128001, 128009])
+    res = {"target": "Llama-3-8B shape (random init, 32 layers)" if layers_8b == 32 else f"Llama-3-8B shape, {layers_8b} layers",
+           "drafter": "Llama-3.2-1B shape (random init, 16 layers)" if layers_1b == 16 else f"Llama-3.2-1B shape, {layers_1b} layers",
+           "dtype": "bf16", "batch": batch, "prompt_len": prompt, "gen_len": gen,
+           "gamma": gamma, "model_build_s": build_s,
+           "note": "random weights: the acceptance rate is meaningless (near-uniform logits); the tokens/s and the "
+                   "hot path's share of the wall time are the measurement. The target runs uncached over the whole "
+                   "sequence every window, as the reference does (engine/infer_engine.py:270-273)."}
+    for mode in modes:
+        set_noise_mode(mode, seed=5) if mode == "philox" else set_noise_mode("stream")
+        torch.manual_seed(3)
+        infer_engine.batch_speculative_generate(ctx, ids, mask, batch)   # warm-up
+        torch.cuda.synchronize()
+        from specdec_amd import noise as nz
+        timer = HotPathTimer([infer_engine])
+        timer.saved.append((nz.StreamNoise, "reserve", nz.StreamNoise.reserve))   # the STREAM word pool
+        nz.StreamNoise.reserve = timer._wrap(nz.StreamNoise.reserve)
+        torch.manual_seed(3)
+        t0 = time.perf_counter()
+        try:
+            outs, rates = infer_engine.batch_speculative_generate(ctx, ids, mask, batch)
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            hot = timer.device_ms() / 1e3
+            n_calls = len(timer.pairs)
+        finally:
+            timer.restore()
+        gen_tokens = sum(len(o) - prompt for o in outs)
+        res[mode] = {"wall_s": wall, "hot_path_device_s": hot, "hot_path_share": hot / wall,
+                     "hot_path_calls": n_calls, "output_tokens": gen_tokens, "tokens_per_s": gen_tokens / wall,
+                     "acceptance_rate_meaningless": sum(rates) / len(rates)}
+        print(json.dumps({mode: res[mode]}), file=sys.stderr, flush=True)
+    set_noise_mode("stream")
+    del target, drafter
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
@@ -80,49 +133,7 @@ def main():
     ap.add_argument("--layers-8b", type=int, default=32)
     ap.add_argument("--layers-1b", type=int, default=16)
     args = ap.parse_args()
-    from specdec_amd import set_noise_mode
-    from specdec_amd.engine import infer_engine
-    t0 = time.time()
-    target = llama(4096, 14336, args.layers_8b, 32, 8)      # Llama-3-8B shape
-    drafter = llama(2048, 8192, args.layers_1b, 32, 8)      # Llama-3.2-1B shape
-    torch.cuda.synchronize()
-    build_s = time.time() - t0
-    g = torch.Generator().manual_seed(1)
-    ids = torch.randint(1000, 120000, (args.batch, args.prompt), generator=g).cuda()
-    mask = torch.ones_like(ids)
-    from types import SimpleNamespace
-    ctx = SimpleNamespace(drafter=drafter, target=target, gamma=args.gamma, gen_len=args.gen,
-                          end_tokens=[128001, 128009])
-    res = {"target": "Llama-3-8B shape (random init)", "drafter": "Llama-3.2-1B shape (random init)",
-           "dtype": "bf16", "batch": args.batch, "prompt_len": args.prompt, "gen_len": args.gen,
-           "gamma": args.gamma, "model_build_s": build_s,
-           "note": "random weights: acceptance is meaningless; the time split and tokens/s are the measurement. "
-                   "The target runs uncached over the whole sequence every window, as the reference does "
-                   "(engine/infer_engine.py:270-273)."}
-    for mode in ("philox", "stream"):
-        set_noise_mode(mode, seed=5) if mode == "philox" else set_noise_mode("stream")
-        torch.manual_seed(3)
-        infer_engine.batch_speculative_generate(ctx, ids, mask, args.batch)   # warm-up
-        torch.cuda.synchronize()
-        from specdec_amd import noise as nz
-        timer = HotPathTimer([infer_engine])
-        timer.saved.append((nz.StreamNoise, "reserve", nz.StreamNoise.reserve))   # the STREAM word pool
-        nz.StreamNoise.reserve = timer._wrap(nz.StreamNoise.reserve)
-        torch.manual_seed(3)
-        t0 = time.perf_counter()
-        outs, rates = infer_engine.batch_speculative_generate(ctx, ids, mask, args.batch)
-        torch.cuda.synchronize()
-        wall = time.perf_counter() - t0
-        hot = timer.device_ms() / 1e3
-        n_calls = len(timer.pairs)
-        timer.restore()
-        gen_tokens = sum(len(o) - args.prompt for o in outs)
-        res[mode] = {"wall_s": wall, "hot_path_device_s": hot, "hot_path_share": hot / wall,
-                     "hot_path_calls": n_calls, "output_tokens": gen_tokens, "tokens_per_s": gen_tokens / wall,
-                     "acceptance_rate_meaningless": sum(rates) / len(rates)}
-        print(json.dumps({mode: res[mode]}), file=sys.stderr, flush=True)
-    set_noise_mode("stream")
-    print(json.dumps(res), flush=True)
+    print(json.dumps(run(args.batch, args.prompt, args.gen, args.gamma, args.layers_8b, args.layers_1b)), flush=True)
 
 
 if __name__ == "__main__":

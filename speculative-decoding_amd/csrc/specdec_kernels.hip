@@ -35,6 +35,10 @@
 namespace sd {
 
 constexpr int kMaxCand = 8;
+// The decide tails' register-held slot loops are sized for γ <= 16 (kFastSlots target rows, 2γ + 1
+// rows per sequence); larger γ (<= SD_MAX_GAMMA) loops over groups of that size or takes the general
+// path (decide_seq's seq_stats branch).
+constexpr int kFastSlots = 17;
 
 struct Decision {
     int32_t n;          // accepted drafts
@@ -621,24 +625,27 @@ __device__ __forceinline__ void seq_stats(const Plan& P, int b, float2* lstat, b
         if (publish) P.rowstat[b * P.slots + s] = ms;
     }
     if (P.n_chunks <= kWave) {
-        // one partial per lane per slot: issue every slot's load of this wave before reducing
-        constexpr int kMaxSlotsPerWave = (2 * SD_MAX_GAMMA + 1 + 3) / 4;
-        float2 v[kMaxSlotsPerWave];
+        // one partial per lane per slot: issue every slot's load of this wave (a group of up to
+        // kGroup slots per wave: 2γ + 1 <= 33 slots in one group) before reducing
+        constexpr int kGroup = (2 * kFastSlots - 1 + 3) / 4;
+        for (int g0 = 0; g0 < P.stat_slots; g0 += kGroup * nw) {
+            float2 v[kGroup];
 #pragma unroll
-        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
-            const int s = w + k * nw;
-            v[k] = (s < P.stat_slots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
-                                                      : make_float2(-INFINITY, 0.f);
-        }
+            for (int k = 0; k < kGroup; ++k) {
+                const int s = g0 + w + k * nw;
+                v[k] = (s < P.stat_slots && lane < P.n_chunks) ? ld_coh(P.part + (int64_t)(b * P.slots + s) * P.n_chunks + lane)
+                                                          : make_float2(-INFINITY, 0.f);
+            }
 #pragma unroll
-        for (int k = 0; k < kMaxSlotsPerWave; ++k) {
-            const int s = w + k * nw;
-            if (s >= P.stat_slots) break;
-            const float m = wave_max(v[k].x);
-            const float sum = wave_sum(v[k].x > -INFINITY ? v[k].y * sd_exp(v[k].x - m) : 0.f);
-            if (lane == 0) {
-                lstat[s] = make_float2(m, sum);
-                if (publish) P.rowstat[b * P.slots + s] = make_float2(m, sum);   // read by later launches only
+            for (int k = 0; k < kGroup; ++k) {
+                const int s = g0 + w + k * nw;
+                if (s >= P.stat_slots) break;
+                const float m = wave_max(v[k].x);
+                const float sum = wave_sum(v[k].x > -INFINITY ? v[k].y * sd_exp(v[k].x - m) : 0.f);
+                if (lane == 0) {
+                    lstat[s] = make_float2(m, sum);
+                    if (publish) P.rowstat[b * P.slots + s] = make_float2(m, sum);   // read by later launches only
+                }
             }
         }
         return;
@@ -716,10 +723,10 @@ __device__ __forceinline__ bool accept_draft(const Plan& P, float p, float q, fl
 }
 
 // The accept rule for one sequence given p(x_i), q(x_i); woff = its first noise word (STREAM).
-// lacc (perf mode, nullable): accept flags of the γ drafts precomputed in parallel (decide_seq)
-// lstop (nullable): per-draft "is a stop token" flags, precomputed alongside lacc
+// accm (has_acc): accept flags of the γ drafts precomputed in parallel, bit i = draft i (k_walk)
+// lstop (nullable): per-draft "is a stop token" flags, precomputed alongside them
 __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float* rq, int64_t woff, int64_t* used_out,
-                              const uint8_t* lacc = nullptr, const uint8_t* lstop = nullptr) {
+                              bool has_acc = false, uint64_t accm = 0, const uint8_t* lstop = nullptr) {
     Decision d{};
     d.stop_index = -1;
     d.noise_off = 0;
@@ -731,7 +738,8 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
         // sampling/speculative_decoding.py:139-145: r = rand(γ'); n = first i with r_i > p_i/q_i
         int n = g;
         for (int i = 0; i < g; ++i) {
-            const bool acc = lacc ? lacc[i] != 0 : accept_draft(P, rp[i], rq[i], draw_uniform(P, b, i, woff + i, &overrun));
+            const bool acc = has_acc ? ((accm >> i) & 1u) != 0
+                                     : accept_draft(P, rp[i], rq[i], draw_uniform(P, b, i, woff + i, &overrun));
             if (!acc && n == g) n = i;
         }
         used = g;
@@ -757,7 +765,8 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
         if (act) {
             d.status = SD_ROW_DONE;
             for (int i = 0; i < g; ++i) {
-                const bool acc = lacc ? lacc[i] != 0 : accept_draft(P, rp[i], rq[i], draw_uniform(P, b, i, woff + used, &overrun));
+                const bool acc = has_acc ? ((accm >> i) & 1u) != 0
+                                         : accept_draft(P, rp[i], rq[i], draw_uniform(P, b, i, woff + used, &overrun));
                 used += 1;
                 if (acc) {
                     d.n += 1;
@@ -897,16 +906,14 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
             for (int bi = tid; bi < nb; bi += blockDim.x) {
                 const int b = b0 + bi;
                 const int64_t woff = off + la[bi] + V2 * lk[bi];
-                uint8_t lacc[SD_MAX_GAMMA];
+                uint64_t accm = 0;   // bit i: draft i accepted
                 bool ovr = false;
                 int64_t used;
-#pragma unroll
-                for (int i = 0; i < SD_MAX_GAMMA; ++i) {
-                    if (i >= g) break;
+                for (int i = 0; i < g; ++i) {
                     const float u = uniform_from_word(lw[lk[bi] * W + la[bi] + i]);
-                    lacc[i] = (spec ? !((double)u > lthr[bi * g + i]) : (double)u < lthr[bi * g + i]) ? 1 : 0;
+                    if (spec ? !((double)u > lthr[bi * g + i]) : (double)u < lthr[bi * g + i]) accm |= 1ull << i;
                 }
-                Decision d = walk_core(P, b, lrp + bi * g, lrq + bi * g, woff, &used, lacc, lstop + bi * g);
+                Decision d = walk_core(P, b, lrp + bi * g, lrq + bi * g, woff, &used, true, accm, lstop + bi * g);
                 const bool sampled = spec ? (d.mode != kModeNone && P.t_stoch) : d.mode == kModeResid;
                 const int64_t n_u = used - (sampled ? V2 : 0);
                 for (int i = 0; i < n_u; ++i) ovr |= woff + i >= P.noise.n_words;
@@ -1022,12 +1029,12 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kThreads / kWave;
     const int i = pf_draft(P);
     if (i >= 0) lstop[i] = pf.stop;
-    if (P.dstats && P.n_chunks <= kWave) {
+    if (P.dstats && P.n_chunks <= kWave && P.n_tslots <= kFastSlots) {
         if (i >= 0) {
             lstat[P.n_tslots + i] = pf.ds;
             if (publish) P.rowstat[b * P.slots + P.n_tslots + i] = pf.ds;
         }
-        constexpr int kMaxSlotsPerWave = (SD_MAX_GAMMA + 1 + 3) / 4;
+        constexpr int kMaxSlotsPerWave = (kFastSlots + 3) / 4;
         float2 v[kMaxSlotsPerWave];
         if (poll_epoch) {   // poll mode: each record re-read until it carries this call's tag (bounded)
             static_assert(kMaxSlotsPerWave <= 5, "ld_coh16x5");
@@ -2335,8 +2342,9 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
         int32_t st = SD_ROW_DONE;
         if (!(ms.y > 0.f) || ms.y != ms.y || ms.y == INFINITY) st |= SD_ROW_INVALID_DIST;   // torch raises
         if (P.t_keep) st |= keep_of(P, r).flags;
-        const int64_t x = cp >= 0 ? (int64_t)l_cand[cp] : -1;
+        int64_t x = cp >= 0 ? (int64_t)l_cand[cp] : -1;
         if (x < 0) st |= SD_ROW_INVALID_DIST;
+        if (st & SD_ROW_INVALID_DIST) x = -1;   // a failed row's token is -1, never a usable index
         P.next_token[r * P.next_token_stride] = x;
         if (P.token_prob) P.token_prob[r] = x >= 0 ? prob_exact<DT>(l_y[cp], ms.x, ms.y, 1.0f / ms.y) : NAN;
         if (P.row_stats) P.row_stats[r] = ms;
@@ -2778,6 +2786,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         int32_t st = SD_ROW_DONE | xstat;
         if (!(S > 0.f) || S != S || S == INFINITY) st |= SD_ROW_INVALID_DIST;   // torch raises
         if (x < 0) st |= SD_ROW_INVALID_DIST;
+        if (st & SD_ROW_INVALID_DIST) x = -1;   // a failed row's token is -1, never a usable index
         if (A.poll) __hip_atomic_store(seq_counter(A.cnt, 2, r), epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         A.next_token[r * A.nt_stride] = x;
         if (A.token_prob) A.token_prob[r] = x >= 0 ? prob_exact<DT>(yx, M, S, 1.0f / S) : NAN;
@@ -2965,7 +2974,8 @@ int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt,
     // poll-mode decide tail: the drafter stats came with the draws (target slots only, one launch)
     sd::Plan Q = P;
     static const bool kp_off = getenv("SD_STATS_POLL") && atoi(getenv("SD_STATS_POLL")) == 0;   // A/B
-    Q.kpoll = TAIL && !kp_off && P.dstats && P.n_chunks <= kWave && P.stat_slots == P.n_tslots && slot_lo == 0 &&
+    Q.kpoll = TAIL && !kp_off && P.dstats && P.n_chunks <= kWave && P.stat_slots == P.n_tslots &&
+              P.n_tslots <= sd::kFastSlots && slot_lo == 0 &&
               slot_cnt == P.stat_slots &&
               sample_poll_ok(P.B, fast ? (const void*)k_stats<DT, true, TAIL> : (const void*)k_stats<DT, false, TAIL>);
     if (fast) SD_LAUNCH((k_stats<DT, true, TAIL>), grid, dim3(kThreads), stream, Q, slot_lo, slot_cnt);

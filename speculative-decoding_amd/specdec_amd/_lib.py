@@ -9,8 +9,8 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 8
-SD_MAX_GAMMA = 16
+SD_ABI_VERSION = 9
+SD_MAX_GAMMA = 32
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 SD_F32, SD_BF16, SD_F16 = 0, 1, 2

@@ -92,7 +92,7 @@ static void workspace_shapes() {
             CHECK(sd_probs_workspace_size(B, V) > 0);
         }
     CHECK(sd_verify_workspace_size(0, 4, 10) == 0);
-    CHECK(sd_verify_workspace_size(1, 17, 10) == 0);
+    CHECK(sd_verify_workspace_size(1, SD_MAX_GAMMA + 1, 10) == 0);
     CHECK(sd_sample_workspace_size(1, 0) == 0);
 }
 

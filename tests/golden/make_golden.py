@@ -60,6 +60,13 @@ SPEC_CASES = [
     ("gpt2like_greedy_g4_fp32", 50257, "fp32", 4, ("greedy", 1.0, 0, 1.0), 32, [50256], False, [0]),
     ("llama_greedy_g4_bf16", 128256, "bf16", 4, ("greedy", 1.0, 0, 1.0), 24, [128001, 128009], False, [0]),
     ("llama_multi_g4_bf16", 128256, "bf16", 4, ("multinomial", 1.0, 0, 1.0), 24, [128001, 128009], False, [0]),
+    # γ beyond 16 (SD_MAX_GAMMA = 32): the reference takes any γ (sampling/speculative_decoding.py:106)
+    ("multi_t1_g20_bf16", 4096, "bf16", 20, ("multinomial", 1.0, 0, 1.0), 64, [1], False, [0, 1]),
+    ("greedy_g32_bf16", 4096, "bf16", 32, ("greedy", 1.0, 0, 1.0), 80, [1], False, [0]),
+    ("nucleus09_g20_bf16", 4096, "bf16", 20, ("nucleus", 1.0, 0, 0.9), 48, [1], False, [0]),
+    # drafter = target + N(0, 0.05^2): drafts are accepted deep into the γ = 24 window
+    ("multi_t1_g24_bf16_close", 4096, "bf16", 24, ("multinomial", 1.0, 0, 1.0), 96, [1], False, [0, 1], 0.05),
+    ("greedy_g32_bf16_close", 4096, "bf16", 32, ("greedy", 1.0, 0, 1.0), 96, [1], False, [0], 0.05),
 ]
 
 # The engine re-feeds the last prompt token to the drafter after its prefill (engine/infer_engine.py:206,231),
@@ -77,6 +84,8 @@ ENGINE_CASES = [
     ("b1_g4_bf16_eos", 4096, "bf16", 1, 4, 40, "likely", [0, 1, 2]),
     ("b4_g4_bf16_refcrash", 4096, "bf16", 4, 4, 16, [1], [0]),
     ("llama_b2_g4_fp32", 128256, "fp32", 2, 4, 12, [128001, 128009], [0]),
+    ("b4_g20_fp32", 2048, "fp32", 4, 20, 48, [1], [0]),
+    ("b3_g32_fp32_eos", 2048, "fp32", 3, 32, 70, "likely", [1]),
 ]
 
 # ngram-assisted loop (rule A11): FakeLM target, the reference's n-gram storages as the drafter
@@ -94,6 +103,7 @@ NGRAM_CASES = [
     ("ng_multi_g4_n3_fp32", 4096, "fp32", ("multi", 3), 4, ("multinomial", 1.0, 0, 1.0), 3, False, 40, [1], [0]),
     ("ng_llama_nucleus_g8", 128256, "bf16", ("multi", 3), 8, ("nucleus", 1.0, 0, 0.9), 3, False, 24,
      [128001, 128009], [0, 1, 2]),
+    ("ng_multi_g20_n3", 4096, "bf16", ("multi", 3), 20, ("multinomial", 1.0, 0, 1.0), 3, False, 60, [1], [0]),
 ]
 
 DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
@@ -128,13 +138,29 @@ def make_processor(lp, kind, T, k, p):
             "topknucleus": lambda: lp.TopKNucleusProcessor(T, k, p)}[kind]()
 
 
-def main():
+def _merge(path, new, only):
+    """--cases: the listed cases' records replace / join the file's, every other record is kept."""
+    if only is None:
+        return new
+    with open(path) as f:
+        old = json.load(f)
+    old.update(new)
+    return old
+
+
+def main(only=None):
+    """only: a set of case names (SPEC / ENGINE / NGRAM) to (re)generate into the existing files;
+    None regenerates everything."""
     speculative_generate, lp, prune_tuple_cache, batch_speculative_generate = _import_reference()
     torch.set_num_threads(min(8, os.cpu_count() or 1))
+    keep = (lambda name: True) if only is None else (lambda name: name in only)
 
     spec = {}
-    for name, V, dt, gamma, (kind, T, k, p), gen_len, eos, skip, seeds in SPEC_CASES:
-        target, drafter = make_pair(V, dtype=DT[dt])
+    for name, V, dt, gamma, (kind, T, k, p), gen_len, eos, skip, seeds, *sg in SPEC_CASES:
+        if not keep(name):
+            continue
+        sigma = sg[0] if sg else 1.0
+        target, drafter = make_pair(V, dtype=DT[dt], sigma=sigma)
         if eos == "likely":
             eos = likely_tokens(target)
         for seed in seeds:
@@ -146,15 +172,18 @@ def main():
                 skip_sample_adjustment=skip)
             spec[f"{name}/s{seed}"] = dict(
                 vocab=V, dtype=dt, gamma=gamma, processor=dict(kind=kind, temperature=T, top_k=k, top_p=p),
-                max_gen_len=gen_len, eos=eos, skip_sample_adjustment=skip, seed=seed, prompt=prompt,
+                max_gen_len=gen_len, eos=eos, skip_sample_adjustment=skip, seed=seed, prompt=prompt, sigma=sigma,
                 target_digest=bank_digest(target), drafter_digest=bank_digest(drafter),
                 tokens=out, acceptance_rate=float(rate))
             print(name, seed, len(out), rate, flush=True)
+    spec = _merge(os.path.join(HERE, "spec_loops.json"), spec, only)
     with open(os.path.join(HERE, "spec_loops.json"), "w") as f:
         json.dump(spec, f, indent=1)
 
     eng = {}
     for name, V, dt, B, gamma, gen_len, ends, seeds, *pm in ENGINE_CASES:
+        if not keep(name):
+            continue
         pos_mult = pm[0] if pm else 0
         target, drafter = make_pair(V, dtype=DT[dt], pos_mult=pos_mult)
         if ends == "likely":
@@ -176,12 +205,15 @@ def main():
                 rec.update(outputs=None, rates=None, raised=f"{type(e).__name__}: {e}")
             eng[f"{name}/s{seed}"] = rec
             print(name, seed, rec["raised"] or [len(o) for o in rec["outputs"]], flush=True)
+    eng = _merge(os.path.join(HERE, "engine_loops.json"), eng, only)
     with open(os.path.join(HERE, "engine_loops.json"), "w") as f:
         json.dump(eng, f, indent=1)
 
     ng = _import_reference_ngram()
     ngl = {}
     for name, V, dt, (skind, sn), gamma, (kind, T, k, p), filler, unknown, gen_len, eos, seeds in NGRAM_CASES:
+        if not keep(name):
+            continue
         # next-token logits depend on the last token only, peaked so sampled continuations repeat
         target, _ = make_pair(V, dtype=DT[dt], pos_mult=0, peak=NGRAM_PEAK)
         if eos == "likely":
@@ -201,8 +233,11 @@ def main():
                 stop_if_unknown=unknown, max_gen_len=gen_len, eos=eos, seed=seed, prompt=prompt,
                 target_digest=bank_digest(target), tokens=out, acceptance_rate=float(rate))
             print(name, seed, len(out), rate, flush=True)
+    ngl = _merge(os.path.join(HERE, "ngram_loops.json"), ngl, only)
     with open(os.path.join(HERE, "ngram_loops.json"), "w") as f:
         json.dump(ngl, f, indent=1)
+    if only is not None:
+        return
 
     # processors on small rows
     from safetensors.torch import save_file
@@ -330,6 +365,8 @@ def make_surface():
 if __name__ == "__main__":
     if "--only" in sys.argv and sys.argv[sys.argv.index("--only") + 1] == "surface":
         make_surface()
+    elif "--cases" in sys.argv:   # e.g. --cases multi_t1_g20_bf16,b4_g20_fp32: merged into the files
+        main(set(sys.argv[sys.argv.index("--cases") + 1].split(",")))
     else:
         main()
         make_surface()

@@ -397,14 +397,14 @@ def make_proc(sd, pp):
 def test_speculative_generate_matches_reference(sd, case):
     from specdec_amd.sampling import speculative_generate
     c = SPEC[case]
-    target, drafter = make_pair(c["vocab"], dtype=DT[c["dtype"]], device=DEV)
+    target, drafter = make_pair(c["vocab"], dtype=DT[c["dtype"]], device=DEV, sigma=c.get("sigma", 1.0))
     eos = c["eos"] if len(c["eos"]) > 1 else c["eos"][0]
     torch.manual_seed(c["seed"])
     out, rate = speculative_generate(c["prompt"], drafter, target, gamma=c["gamma"],
                                      logits_processor=make_proc(sd, c["processor"]), max_gen_len=c["max_gen_len"],
                                      eos_tokens_id=eos, skip_sample_adjustment=c["skip_sample_adjustment"])
     if (out, rate) != (c["tokens"], c["acceptance_rate"]):
-        tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]])
+        tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]], sigma=c.get("sigma", 1.0))
         pp = c["processor"]
         match = []
         for label, pv, exact in oracle_variants(ref.Processor(pp["kind"], pp["temperature"], pp["top_k"],

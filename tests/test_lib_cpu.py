@@ -84,7 +84,8 @@ def test_workspace_sizes_are_positive_and_reject_bad_shapes():
     from specdec_amd._lib import lib
     assert lib.sd_verify_workspace_size(32, 4, 128256) > 0
     assert lib.sd_verify_workspace_size(0, 4, 128256) == 0
-    assert lib.sd_verify_workspace_size(1, 17, 128256) == 0
+    assert lib.sd_verify_workspace_size(1, 32, 128256) > 0
+    assert lib.sd_verify_workspace_size(1, 33, 128256) == 0
     assert lib.sd_sample_workspace_size(4, 50257) > 0
 
 

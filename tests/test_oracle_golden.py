@@ -22,17 +22,17 @@ with open(os.path.join(GOLD, "ngram_loops.json")) as f:
 _pairs = {}
 
 
-def pair(V, dt, pos_mult=7):
-    key = (V, dt, pos_mult)
+def pair(V, dt, pos_mult=7, sigma=1.0):
+    key = (V, dt, pos_mult, sigma)
     if key not in _pairs:
-        _pairs[key] = make_pair(V, dtype=DT[dt], pos_mult=pos_mult)
+        _pairs[key] = make_pair(V, dtype=DT[dt], pos_mult=pos_mult, sigma=sigma)
     return _pairs[key]
 
 
 @pytest.mark.parametrize("case", sorted(SPEC))
 def test_spec_loop_matches_reference(case):
     c = SPEC[case]
-    target, drafter = pair(c["vocab"], c["dtype"])
+    target, drafter = pair(c["vocab"], c["dtype"], sigma=c.get("sigma", 1.0))
     assert bank_digest(target) == c["target_digest"] and bank_digest(drafter) == c["drafter_digest"]
     pp = c["processor"]
     proc = ref.Processor(pp["kind"], pp["temperature"], pp["top_k"], pp["top_p"])
