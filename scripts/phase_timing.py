@@ -59,7 +59,8 @@ for rep in range(3):
     t = ts.view(-1, 16).cpu().numpy().astype(np.int64)
     print(f"--- rep {rep}")
     for name, lo, hi, phases in (("k_stats", 0, 8192, ["start", "merged", "arrived", "decided", "dec_stats", "dec_ratios",
-                                                        "stream_done", "pf_late", "rec_stored"]
+                                                        "stream_done", "pf_late", "rec_stored", "dec_polled",
+                                                        "-", "dec_tags_ok"]
                    if not LEAN else ["start", "merged", "rec_stored", "decided", "accepts", "-",
                                      "loads_landed", "rows_reduced"]),
                                  ("k_sample_finish", 16384 - 64, 16384, ["start", "prologue", "body_end", "arrived",
@@ -67,7 +68,7 @@ for rep in range(3):
                                                             "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"]),
                                  ("k_sample", 8192, 16384 - 64, ["start", "prologue", "body_end", "arrived",
                                                             "tail_S", "cdf_pick", "finalized", "cdf_select",
-                                                            "cdf_loaded", "cdf_wscan", "cdf_found", "cdf_1st"])):
+                                                            "weights", "chunk_pick", "-", "-"])):
         blk = t[lo:hi]
         blk = blk[blk[:, 0] > 0]
         if not len(blk):
@@ -80,6 +81,29 @@ for rep in range(3):
             if len(v):
                 d = (v - t0) / 100.0
                 print(f"  {ph:10s} n={len(v):5d}  min {d.min():7.2f}  p50 {np.median(d):7.2f}  max {d.max():7.2f} us")
+    # the fused verify (k_verify_fused, B >= 8): spans + a decider per sequence, then the samplers
+    nsp = 16 if not SPEC else 20
+    head = B * (nsp + 1)
+    blk = t[:8192]
+    if (blk[head:, 0] > 0).any() and not LEAN:
+        t0 = blk[blk[:, 0] > 0, 0].min()
+        d = (blk - t0) / 100.0
+        d[blk == 0] = np.nan
+        wgi = np.arange(8192)
+        item = (wgi >> 3) % (nsp + 1)
+        roles = {"span": (wgi < head) & (item < nsp), "decider": (wgi < head) & (item == nsp),
+                 "sampler": (wgi >= head) & (blk[:, 0] > 0)}
+        names = {"span": {0: "start", 6: "stream_done", 1: "merged", 8: "rec_stored"},
+                 "decider": {0: "start", 7: "pf_done", 9: "polled", 11: "tags_ok", 3: "decided", 4: "tail_S",
+                             6: "finalized"},
+                 "sampler": {0: "start", 1: "saw_decision", 8: "weights", 9: "chunk_pick", 2: "done"}}
+        print("fused verify roles:")
+        for r, m in roles.items():
+            for col, nm in names[r].items():
+                v = d[m, col]
+                v = v[~np.isnan(v)]
+                if len(v):
+                    print(f"  {r:8s} {nm:13s} n={len(v):5d}  min {v.min():7.2f}  p50 {np.median(v):7.2f}  max {v.max():7.2f} us")
     if rep == 2:   # per-workgroup dump of the k_stats launch for offline analysis
         np.save(os.path.join(ROOT, "gpurun_out", "phase_kstats.npy"), t[:8192])
     blk = t[8192:16384]

@@ -110,6 +110,9 @@ struct Plan {
     Decision* dec;
     ResPart* rpart;
     uint4* srec;          // k_stats' poll-mode records: rpart, or past the sampler's records (k_verify_lean)
+    uint4* sprec;         // sampling-chunk records {Σw, Σp, candidate, tag} (sample_chunk): rpart, or past srec (fused)
+    uint4* drec;          // fused verify: per sequence two tagged decision records for its samplers
+    int32_t n_samp;       // fused verify (k_stats<.., SAMP>): sampling workgroups per sequence
     int32_t* keep_hist;   // threshold scratch
     uint32_t* thr_part;   // 16-bit thresholds (sd_threshold.inc): per (row, slice) max key | NaN-inf flag
     float* thr_tail;      //   per (row, slice) Σexp below the window / tie counts
@@ -160,6 +163,7 @@ struct Plan {
 // counters sharing a line would serialise every sequence's arrivals on it.
 constexpr int kCntMax = 16384;
 constexpr int kTailChunks = 1024;   // perf-mode sampling: chunk partials staged in LDS (V <= 2 Mi)
+constexpr int32_t kLostDecision = -2;   // fused verify: a sampler's record when the decision never arrived
 constexpr int kCntStride = 32;   // uint32 words per counter (128 B)
 __device__ __forceinline__ uint32_t* seq_counter(const uint32_t* base, int set, int b) {
     return const_cast<uint32_t*>(base) + ((size_t)set * kCntMax + b) * kCntStride;
@@ -380,10 +384,19 @@ __device__ __forceinline__ void affine_split(int id, int per_seq, int& b, int& i
     item = k % per_seq;
 }
 
+template <int DT, bool FAST>
+__device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int wg_id);
+template <int DT, bool FAST>
+__device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decision& d, uint32_t epoch, int wg_id);
+
 // <= 80 SGPRs keeps 8 workgroups of 256 threads resident per CU (MI355X_MICROARCH.md, residency)
 // TAIL (perf mode): the last workgroup to finish a sequence's rows runs its decision (decide_seq).
-template <int DT, bool FAST, bool TAIL>
-__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot_lo, int slot_cnt) {
+// SAMP (perf mode, poll, stochastic target rows): the whole verify in this launch — per sequence
+// P.n_samp sampling workgroups poll the decider's decision records, draw their chunk's candidate of
+// the decided row and publish it; the decider then polls those records and finishes (the token, the
+// outputs, the engine state): no k_sample launch, no kernel boundary, no decision reload.
+template <int DT, bool FAST, bool TAIL, bool SAMP>
+__device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_cnt) {
     __shared__ float lm[4], ls[4];
     constexpr int VEC = Elem<DT>::kVec;
     constexpr int STEP = kThreads * VEC;                      // elements per workgroup stage
@@ -393,17 +406,66 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     // branch between them, both row tables indexed unconditionally): the scalar loads then go out
     // together with one wait, instead of a chain of ~10 dependent waits that put the first row
     // load ~3 us after the start at batch 1.
-    const int gx = (int)gridDim.x;
+    const int gx = P.n_chunks;
     const int xa = P.xcd_affine, nt = P.n_tslots;
     const int64_t tstr = P.tstride, dstr = P.dstride;
+    // poll mode (TAIL): a 1-D grid of B x (slot_cnt x n_chunks + 1) workgroups — per sequence its
+    // streaming spans and one DECIDER, which streams nothing: it prefetches the drafts' inputs while
+    // the spans stream, polls their records and decides.  Counter mode: (n_chunks, B x slot_cnt), the
+    // last arrival decides.
+    const bool poll = TAIL && P.kpoll;
+    const int n_span = slot_cnt * gx;
+    const int per_seq = n_span + (poll ? 1 : 0);
     int b, s, chunk;
-    {
-        int ba, item;
-        affine_split(wg_id, slot_cnt * gx, ba, item);
-        const int bn = (int)blockIdx.y / slot_cnt, sn = slot_lo + (int)blockIdx.y % slot_cnt;
-        b = xa ? ba : bn;
-        s = xa ? slot_lo + item / gx : sn;
-        chunk = xa ? item % gx : (int)blockIdx.x;
+    bool decider = false;
+    int samp = -1;
+    if (SAMP && wg_id >= P.B * per_seq) {
+        // the samplers come after every span and decider in dispatch order (block id): they only wait
+        // for a decision, so the spans, which wait for nothing, always get their slots first, and a
+        // sampler frees its slot once it has published.  Sequence b = id % B: with B % 8 == 0 every
+        // workgroup of a sequence sits on one XCD group (affine_split's rule)
+        const int t = wg_id - P.B * per_seq;
+        b = t % P.B;
+        samp = t / P.B;
+        s = slot_lo;
+        chunk = 0;
+    } else {
+        int item;
+        if (xa) affine_split(wg_id, per_seq, b, item);
+        else { b = wg_id / per_seq; item = wg_id - b * per_seq; }
+        decider = poll && item == n_span;
+        s = slot_lo + (item < n_span ? item / gx : 0);
+        chunk = item < n_span ? item % gx : 0;
+    }
+    if constexpr (SAMP) {
+        if (samp >= 0) {
+            fused_sampler<DT, FAST>(P, b, samp, wg_id);
+            return;
+        }
+    }
+    __shared__ uint32_t s_epoch;
+    if (TAIL && decider) {
+        // the drafts' ids, logits, drafter stats, stop flags and accept uniforms while the spans stream
+        DraftPf pf;
+        const int pi = pf_draft(P);
+        pf_early(P, b, pi, pf);
+        if (threadIdx.x == 0) s_epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pf_late(P, b, pi, pf);
+        __syncthreads();
+        SD_TS(wg_id, 7);
+        if constexpr (SAMP) {
+            __shared__ Decision s_dec;
+            decide_seq(P, b, pf, wg_id, &s_dec, true, true, &s_epoch);
+            __syncthreads();
+            SD_TS(wg_id, 3);
+            fused_finish<DT, FAST>(P, b, s_dec, s_epoch, wg_id);
+        } else {
+            decide_seq(P, b, pf, wg_id, nullptr, true, true, &s_epoch);
+            SD_TS(wg_id, 3);
+        }
+        if (threadIdx.x == 0)   // every span has read the epoch (its record carries it): advance it
+            __hip_atomic_store(seq_counter(P.cnt, 3, b), s_epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
     }
     const bool is_t = s < nt;
     const char* tp = static_cast<const char*>(P.trow[is_t ? s : 0]);
@@ -413,21 +475,18 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     // poll mode: this call's epoch of sequence b (thread 0), issued AFTER the first row loads and
     // kept in a register until the record: loads complete in order, so an atomic issued first
     // held back the wave's first stage (batch 1: stream done 3.2 vs ~1.4 us after the start)
-    __shared__ uint32_t s_epoch;
-    const bool ep_thread = TAIL && P.kpoll && threadIdx.x == 0;
+    const bool ep_thread = poll && threadIdx.x == 0;
     uint32_t ep_reg = 0u;
     bool ep_read = false;
     auto read_epoch = [&]() {
         if (ep_thread && !ep_read) ep_reg = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ep_read = true;
     };
-    // TAIL: drafted ids now (consumed after the loop), their logits right after it, so a
-    // workgroup that turns out to be its sequence's last arrival has them in registers.  Poll mode
-    // knows its consumer up front (the last span of the last slot): the producers skip the
-    // prefetch, whose dependent loads the workgroup barrier below would wait for before their
-    // records go out (batch 1: records at 5.8 instead of ~2 us after the launch)
+    // TAIL, counter mode: drafted ids now (consumed after the loop), their logits right after it,
+    // so a workgroup that turns out to be its sequence's last arrival has them in registers.  Poll
+    // mode: the decider prefetches them; the spans only stream
     DraftPf pf;
-    const bool pf_here = TAIL && (!P.kpoll || (s == P.stat_slots - 1 && chunk == P.n_chunks - 1));
+    const bool pf_here = TAIL && !poll;
     const int pf_i = pf_here ? pf_draft(P) : -1;
     if (TAIL) pf_early(P, b, pf_i, pf);
     const float T = is_t ? P.tT : P.dT;
@@ -497,6 +556,11 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     // unconditionally (the prefetch index is clamped), so the compiler keeps kPipe of them in
     // flight with counted vmcnt waits instead of draining to vmcnt(0) each stage.
     const int nfull = aligned ? cnt - (last_partial ? 1 : 0) : 0;
+    // the row's ragged last stage (aligned rows): one clamped vector per lane, loaded up front
+    const bool vtail = aligned && last_partial && P.V >= VEC;
+    const int64_t tail_e0 = vtail ? stage_of(cnt - 1) * STEP + threadIdx.x * VEC : 0;
+    uint4 tailv = make_uint4(0u, 0u, 0u, 0u);
+    if (vtail) tailv = ld16_clamped<DT>(row, tail_e0, last_whole_vec<DT>(P.V));
     if (nfull > 0) {
         const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;   // stage k at vb[k * kThreads]
         uint4 buf[kPipe];
@@ -524,8 +588,13 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
             }
         }
     }
-    // the row's partial last stage (and misaligned rows): guarded element loads
-    for (int it = nfull; it < cnt; ++it) {
+    if (vtail) {
+        float x[VEC];
+        finish16<DT>(tailv, row, tail_e0, P.V, x);
+        consume(x, tail_e0, std::true_type{});
+    }
+    // misaligned rows: guarded element loads
+    for (int it = vtail ? cnt : nfull; it < cnt; ++it) {
         const int64_t e0 = stage_of(it) * STEP + threadIdx.x * VEC;
         float x[VEC];
 #pragma unroll
@@ -537,26 +606,28 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     SD_TS(wg_id, 6);
     if (TAIL) pf_late(P, b, pf_i, pf);
     SD_TS(wg_id, 7);
-    // workgroup combine (fixed order): DPP wave merge, then the 4 waves through LDS
-    merge_step<kDppQuad1032>(m, acc);
-    merge_step<kDppQuad2301>(m, acc);
-    merge_step<kDppRowHalfMirror>(m, acc);
-    merge_step<kDppRowMirror>(m, acc);
-    merge_step<kDppRowBcast15, 0xA>(m, acc);
-    merge_step<kDppRowBcast31, 0xC>(m, acc);
-    m = lane63_f(m);
-    acc = lane63_f(acc);
+    // workgroup combine (fixed order): the wave's max, every lane's sum rescaled to it, one wave sum;
+    // then the 4 waves through LDS.  A NaN sum stays NaN; lanes of only -inf add nothing.
+    {
+        const float mw = wave_max(m);
+        const float sc = m > -INFINITY ? acc * sd_exp(m - mw) : (acc != acc ? acc : 0.f);
+        acc = wave_sum(sc);
+        m = mw;
+    }
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (lane == 0) { lm[w] = m; ls[w] = acc; }
     __syncthreads();
     SD_TS(wg_id, 1);
-    // poll mode (TAIL): one tagged 16-byte record per (slot, span); the sequence's last span of its
-    // last slot (the ragged one) is the consumer: it polls the records and decides — no counter.
-    // Counter mode: the (m, S) partial and an arrival; the last arrival decides.
-    const bool poll = TAIL && P.kpoll;
+    // poll mode (TAIL): one tagged 16-byte record per (slot, span), polled by the sequence's decider
+    // — no counter.  Counter mode: the (m, S) partial and an arrival; the last arrival decides.
     if (threadIdx.x == 0) {
-        float M = lm[0], S = ls[0];
-        for (int k = 1; k < kThreads / kWave; ++k) online_merge(M, S, lm[k], ls[k]);
+        constexpr int NW = kThreads / kWave;
+        float M = lm[0];
+#pragma unroll
+        for (int k = 1; k < NW; ++k) M = fmaxf(M, lm[k]);
+        float S = 0.f;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) S += lm[k] > -INFINITY ? ls[k] * sd_exp(lm[k] - M) : (ls[k] != ls[k] ? ls[k] : 0.f);
         if (poll)
             st_coh16(stats_rec(P, b, s, chunk), make_uint4(__float_as_uint(M), __float_as_uint(S),
                                                            stats_tag(s_epoch, b, s, chunk), 0u));
@@ -565,20 +636,27 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
     }
     SD_TS(wg_id, 8);
     if constexpr (TAIL) {
+        if (poll) return;   // the decider takes it from the records
         __shared__ int s_last;
-        if (poll) {
-            if (s != P.stat_slots - 1 || chunk != P.n_chunks - 1) return;
-        } else {
-            if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.stat_slots * P.n_chunks));
-            __syncthreads();
-            SD_TS(wg_id, 2);
-            if (!s_last) return;
-        }
-        decide_seq(P, b, pf, wg_id, nullptr, true, true, poll ? &s_epoch : nullptr);
+        if (threadIdx.x == 0) s_last = arrive_last(seq_counter(P.cnt, 0, b), (uint32_t)(P.stat_slots * P.n_chunks));
+        __syncthreads();
+        SD_TS(wg_id, 2);
+        if (!s_last) return;
+        decide_seq(P, b, pf, wg_id, nullptr, true, true, nullptr);
         SD_TS(wg_id, 3);
-        if (poll && threadIdx.x == 0)
-            __hip_atomic_store(seq_counter(P.cnt, 3, b), s_epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+}
+
+template <int DT, bool FAST, bool TAIL>
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot_lo, int slot_cnt) {
+    stats_body<DT, FAST, TAIL, false>(P, slot_lo, slot_cnt);
+}
+
+// The fused verify (stats_body with SAMP): grid = B x (spans + decider) then B x n_samp samplers (two
+// 2048-element chunks each)
+template <int DT, bool FAST>
+__global__ void __launch_bounds__(kThreads, 7) SD_SGPR_CAP k_verify_fused(Plan P, int slot_lo, int slot_cnt) {
+    stats_body<DT, FAST, true, true>(P, slot_lo, slot_cnt);
 }
 
 // combine the chunk partials of row r (one wave)
@@ -1613,6 +1691,10 @@ struct PairVec {
     static constexpr int kVec = Elem<TDT>::kVec < Elem<DDT>::kVec ? Elem<TDT>::kVec : Elem<DDT>::kVec;
 };
 
+template <int TDT, int DDT, bool FAST>
+__device__ __forceinline__ void pair_weights_from(const PairRows& R, int64_t e0, const float* xt, const float* xd,
+                                                  float* w, float* pw);
+
 // weights of the VEC elements starting at e0 (0 past the vocabulary)
 template <int TDT, int DDT, bool FAST>
 __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, float* w, float* pw = nullptr) {
@@ -1631,6 +1713,14 @@ __device__ __forceinline__ void pair_weights(const PairRows& R, int64_t e0, floa
             load_vecn<DDT, VEC>(R.drow, e0, R.V, R.d_al, xd);   // dprobs dispatches DDT = F32
         }
     }
+    pair_weights_from<TDT, DDT, FAST>(R, e0, xt, xd, w, pw);
+}
+
+// the weights of pair_weights from the loaded values
+template <int TDT, int DDT, bool FAST>
+__device__ __forceinline__ void pair_weights_from(const PairRows& R, int64_t e0, const float* xt, const float* xd,
+                                                  float* w, float* pw) {
+    constexpr int VEC = PairVec<TDT, DDT>::kVec;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
         const int64_t j = e0 + k;
@@ -1800,10 +1890,9 @@ __device__ __forceinline__ int pick_chunk(const Plan& P, double u, const float* 
 // argmax-candidate pick for greedy ones; then the outputs and the engine state.  One memory round
 // trip: engine-state read issued first, every chunk partial staged into LDS in one cooperative
 // load.  Only the engine's den <= 1e-12 fallback re-reads a chunk (its p weights).
-template <int TDT, int DDT, bool FAST, bool STOCH>
+template <int TDT, int DDT, bool FAST, bool STOCH, int EPT = 8>
 __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, int b, PairRows R, double u_row,
                                               int wg_id, const uint32_t* poll_epoch = nullptr) {
-    constexpr int EPT = 8;
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const bool engine_state = P.rule == SD_RULE_ENGINE && P.generated != nullptr;
     int64_t acc0 = 0;
@@ -1823,7 +1912,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
         __shared__ int32_t l_cand[kTailChunks];
         __shared__ float s_mass;
         if (d.mode != kModeNone) {
-            const float4* rp = reinterpret_cast<const float4*>(P.rpart) + (int64_t)b * P.rn_chunks;
+            const float4* rp = reinterpret_cast<const float4*>(P.sprec) + (int64_t)b * P.rn_chunks;
             for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
                 uint4 v = ld_coh16(rp + k);
                 if (poll_epoch) {   // poll mode: re-read until the record carries this call's tag (bounded)
@@ -1837,6 +1926,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
                 l_sum[k] = __uint_as_float(v.x);
                 l_pv[k] = __uint_as_float(v.y);
                 l_cand[k] = (int32_t)v.z;
+                if ((int32_t)v.z == kLostDecision) atomicOr(&s_xstat, SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST);
             }
             if (stop_lane) lstops[threadIdx.x] = stop_v;
             __syncthreads();
@@ -1895,9 +1985,24 @@ __device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
 // Stochastic sampling chunk c of sequence b (whole workgroup): the chunk's Σ weight, Σ p, and its own
 // inverse-CDF candidate (pick_chunk's comment), published as one 16-byte record (k_draw's layout;
 // .w = the poll-mode tag, or 0).
-template <int TDT, int DDT, bool FAST>
-__device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, int b, int c, uint32_t tag) {
-    constexpr int EPT = 8;
+// chunk c's draw from weights already in registers (sample_chunk's second half)
+template <int TDT, int DDT, int EPT>
+__device__ __forceinline__ void sample_chunk_pick(const Plan& P, int b, int c, const float* wv, float psum, uint32_t tag,
+                                                  int wg_id) {
+    const double u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
+    const int64_t base = (int64_t)c * P.rchunk;
+    double T;
+    float PT;
+    const int pos = chunk_pick<EPT>(wv, u, psum, T, PT);
+    SD_TS(wg_id, 9);
+    if (threadIdx.x == 0)   // {Σ w, Σ p, candidate, tag}
+        st_coh16(reinterpret_cast<float4*>(P.sprec) + (int64_t)b * P.rn_chunks + c,
+                 make_uint4(__float_as_uint((float)T), __float_as_uint(PT),
+                            (uint32_t)(pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos)), tag));
+}
+
+template <int TDT, int DDT, bool FAST, int EPT = 8>
+__device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, int b, int c, uint32_t tag, int wg_id = 0) {
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
     const double u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
     float psum = 0.f;
@@ -1910,11 +2015,13 @@ __device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, i
 #pragma unroll
         for (int k = 0; k < VEC; ++k) psum += pv[k];
     }
+    SD_TS(wg_id, 8);
     double T;
     float PT;
     const int pos = chunk_pick<EPT>(wv, u, psum, T, PT);
+    SD_TS(wg_id, 9);
     if (threadIdx.x == 0)   // {Σ w, Σ p, candidate, tag}
-        st_coh16(reinterpret_cast<float4*>(P.rpart) + (int64_t)b * P.rn_chunks + c,
+        st_coh16(reinterpret_cast<float4*>(P.sprec) + (int64_t)b * P.rn_chunks + c,
                  make_uint4(__float_as_uint((float)T), __float_as_uint(PT),
                             (uint32_t)(pos < 0 ? -1 : (int32_t)chunk_elem<TDT, DDT, EPT>(base, pos)), tag));
 }
@@ -1962,7 +2069,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
             // RESID also sums p: the engine's den <= 1e-12 fallback samples the target row itself
             R = pair_rows<TDT, DDT>(P, d, b);
             SD_TS(wg_id, 1);
-            sample_chunk<TDT, DDT, FAST>(P, R, b, c, poll ? sample_tag(epoch, b, c) : 0u);
+            sample_chunk<TDT, DDT, FAST>(P, R, b, c, poll ? sample_tag(epoch, b, c) : 0u, wg_id);
         } else {
             const float2 mst = P.rowstat[b * P.slots + d.slot];
             const float2 msd = d.mode == kModeResid && !P.draft_is_probs ? P.rowstat[b * P.slots + P.n_tslots + d.slot]
@@ -2004,6 +2111,145 @@ __global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
     if (STOCH && d.mode != kModeNone) R = pair_rows<TDT, DDT>(P, d, b);
     SD_TS(16384 - 1 - b, 1);
     sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, STOCH ? cdf_uniform(P.noise, (uint32_t)b) : 0.0, 16384 - 1 - b);
+}
+
+// ------------------------------------------------------------------ fused verify (k_stats<.., SAMP>)
+// The decider hands its decision to the sequence's sampling workgroups as two tagged 16-byte records
+// (k_draw_lean's protocol: write-through stores, each record validated by its own tag):
+//   A = {mode | slot << 8, mst.x, mst.y, tag}, B = {msd.x, msd.y, 0, tag}.
+// A sampler publishes its chunk record (sample_chunk) — or, for a sequence with nothing to sample,
+// an empty one — so the decider always waits for every sampler before it advances the epoch.
+constexpr int kFusedEpt = 8;                       // k_sample's chunking: 2048-element chunks, the same draws
+
+__device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
+    uint32_t h = epoch * 0x9E3779B1u + (uint32_t)b * 0x85EBCA77u + (uint32_t)k * 0xC2B2AE3Du + 0x1B873593u;
+    h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;   // murmur3 fmix32
+    return h | 1u;
+}
+
+template <int DT, bool FAST>
+__device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int wg_id) {
+    __shared__ uint4 s_rec[2];
+    __shared__ uint32_t s_ep;
+    __shared__ int32_t s_ok;
+    SD_TS(wg_id, 0);
+    if (threadIdx.x < kWave) {
+        const int lane = threadIdx.x;
+        uint32_t ep = 0;
+        if (lane == 0) ep = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ep = __builtin_amdgcn_readfirstlane(ep);
+        bool have = lane >= 2;
+        uint4 r = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t tag = lane < 2 ? dec_tag(ep, b, lane) : 0u;
+        for (int spin = 0;; ++spin) {
+            if (!have) {
+                r = ld_coh16(P.drec + 2 * b + lane);
+                have = r.w == tag;
+            }
+            if (__all(have)) break;
+            if (!spin_more(spin, P.spin_limit)) break;   // bounded: the finisher flags the row
+            __builtin_amdgcn_s_sleep(2);   // ~128 clocks: the decision is microseconds away
+        }
+        if (lane < 2) s_rec[lane] = r;
+        if (lane == 0) { s_ep = ep; s_ok = __all(have) ? 1 : 0; }
+    }
+    __syncthreads();
+    SD_TS(wg_id, 1);
+    const uint32_t ep = s_ep;
+    const uint4 A = s_rec[0], Bq = s_rec[1];
+    Decision d{};
+    d.mode = (int32_t)(A.x & 0xffu);
+    d.slot = (int32_t)(A.x >> 8);
+    d.mst = make_float2(__uint_as_float(A.y), __uint_as_float(A.z));
+    d.msd = make_float2(__uint_as_float(Bq.x), __uint_as_float(Bq.y));
+    const bool ok = s_ok != 0;
+    if (!ok || d.mode <= kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) {
+        // nothing to draw (or the decision was lost): empty records for both chunks
+        if (threadIdx.x < 2 && 2 * c + (int)threadIdx.x < P.rn_chunks) {
+            const int cc = 2 * c + (int)threadIdx.x;
+            st_coh16(reinterpret_cast<float4*>(P.sprec) + (int64_t)b * P.rn_chunks + cc,
+                     make_uint4(0u, 0u, (uint32_t)(ok ? -1 : kLostDecision), sample_tag(ep, b, cc)));
+        }
+        return;
+    }
+    const PairRows R = pair_rows<DT, DT>(P, d, b);
+    // chunks 2c and 2c + 1 of the decided rows: every vector of both in flight at once, then each
+    // chunk's weights and draw (k_sample's chunking and uniforms: the same draws)
+    constexpr int VEC = Elem<DT>::kVec, NV = kFusedEpt / VEC;
+    const int c0 = 2 * c, c1 = 2 * c + 1;
+    const bool has1 = c1 < P.rn_chunks;
+    if (!(R.t_al && (!R.resid || R.d_al) && P.V >= VEC)) {   // misaligned rows: one chunk at a time
+        sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c0, sample_tag(ep, b, c0), wg_id);
+        if (has1) sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c1, sample_tag(ep, b, c1), wg_id);
+        return;
+    }
+    const int64_t lastv = last_whole_vec<DT>(P.V);
+    uint4 rt[NV], rd[NV];
+    auto issue = [&](int cc) {
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t e0 = (int64_t)cc * P.rchunk + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+            rt[v] = ld16_clamped<DT>(R.trow, e0, lastv);
+            rd[v] = R.resid ? ld16_clamped<DT>(R.drow, e0, lastv) : make_uint4(0u, 0u, 0u, 0u);
+        }
+    };
+    auto weights = [&](int cc, float* wv, float& psum) {
+        psum = 0.f;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int64_t e0 = (int64_t)cc * P.rchunk + ((int64_t)v * kThreads + threadIdx.x) * VEC;
+            float xt[VEC], xd[VEC], pv[VEC];
+            finish16<DT>(rt[v], R.trow, e0, P.V, xt);
+            if (R.resid) finish16<DT>(rd[v], R.drow, e0, P.V, xd);
+            pair_weights_from<DT, DT, FAST>(R, e0, xt, xd, wv + v * VEC, pv);
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) psum += pv[k];
+        }
+    };
+    // chunk c0's vectors, its weights, then chunk c1's loads go out before c0's draw (its barriers
+    // and scans) so they land meanwhile; only the weights of one chunk and the raw vectors of the
+    // other are live together
+    float wv[kFusedEpt], psum;
+    issue(c0);
+    weights(c0, wv, psum);
+    if (NV == 1 && has1) issue(c1);   // fp32 rows (two vectors per chunk): after the draw, no spills
+    SD_TS(wg_id, 8);
+    sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id);
+    if (has1) {
+        if (NV != 1) issue(c1);
+        weights(c1, wv, psum);
+        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id);
+    }
+    SD_TS(wg_id, 2);
+}
+
+// The decider after deciding (whole workgroup): the decision records for the samplers, then their
+// chunk records (always every one of them, so none is left polling an advanced epoch) and the
+// token / outputs as k_sample's tail writes them.
+template <int DT, bool FAST>
+__device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decision& d0, uint32_t epoch, int wg_id) {
+    Decision d = d0;
+    if (d.mode < kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) d.mode = kModeNone;
+    if (threadIdx.x == 0) {
+        const uint32_t mslot = (uint32_t)(d.mode & 0xff) | ((uint32_t)(d.mode != kModeNone ? d.slot : 0) << 8);
+        st_coh16(P.drec + 2 * b, make_uint4(mslot, __float_as_uint(d.mst.x), __float_as_uint(d.mst.y), dec_tag(epoch, b, 0)));
+        st_coh16(P.drec + 2 * b + 1, make_uint4(__float_as_uint(d.msd.x), __float_as_uint(d.msd.y), 0u, dec_tag(epoch, b, 1)));
+    }
+    const double u_row = cdf_uniform(P.noise, (uint32_t)b);   // the chunk pick's uniform, before the wait
+    PairRows R{};
+    if (d.mode != kModeNone) R = pair_rows<DT, DT>(P, d, b);
+    if (d.mode == kModeNone) {
+        // every sampler's (empty) record before the epoch moves on
+        const float4* rp = reinterpret_cast<const float4*>(P.sprec) + (int64_t)b * P.rn_chunks;
+        for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
+            const uint32_t tag = sample_tag(epoch, b, k);
+            for (int spin = 0; ld_coh16(rp + k).w != tag && spin_more(spin, P.spin_limit); ++spin)
+                __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __shared__ uint32_t s_ep2;
+    if (threadIdx.x == 0) s_ep2 = epoch;
+    sample_finish<DT, DT, FAST, true, kFusedEpt>(P, d, b, R, u_row, wg_id, &s_ep2);
 }
 
 // ------------------------------------------------------------------ sd_sample kernels
@@ -2910,6 +3156,9 @@ void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     // + 1 per row: room for 16-byte records padded to whole 128-B lines per row (k_draw_lean)
     P.rpart = c.take<ResPart>((size_t)(B > rows_total ? B : rows_total) * (nc + 1));
     P.srec = reinterpret_cast<uint4*>(P.rpart);
+    P.sprec = reinterpret_cast<uint4*>(P.rpart);
+    P.drec = nullptr;
+    P.n_samp = 0;
     P.keep_hist = c.take<int32_t>((size_t)rows_total * kThreshScratchInts);
     P.thr_part = c.take<uint32_t>((size_t)rows_total * kThrMaxSlices);
     P.thr_tail = c.take<float>((size_t)rows_total * kThrMaxSlices);
@@ -2978,9 +3227,53 @@ int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt,
               P.n_tslots <= sd::kFastSlots && slot_lo == 0 &&
               slot_cnt == P.stat_slots &&
               sample_poll_ok(P.B, fast ? (const void*)k_stats<DT, true, TAIL> : (const void*)k_stats<DT, false, TAIL>);
-    if (fast) SD_LAUNCH((k_stats<DT, true, TAIL>), grid, dim3(kThreads), stream, Q, slot_lo, slot_cnt);
-    else SD_LAUNCH((k_stats<DT, false, TAIL>), grid, dim3(kThreads), stream, Q, slot_lo, slot_cnt);
+    // poll mode: a 1-D grid with one decider workgroup per sequence after its spans (k_stats)
+    const dim3 g2 = Q.kpoll ? dim3(P.B * (slot_cnt * P.n_chunks + 1)) : grid;
+    if (fast) SD_LAUNCH((k_stats<DT, true, TAIL>), g2, dim3(kThreads), stream, Q, slot_lo, slot_cnt);
+    else SD_LAUNCH((k_stats<DT, false, TAIL>), g2, dim3(kThreads), stream, Q, slot_lo, slot_cnt);
     return SD_OK;
+}
+
+// resident capacity of a kernel's 256-thread workgroups on this device (occupancy x CUs), cached
+int resident_cap(const void* kern) {
+    static std::mutex mu;
+    static std::map<std::pair<int, const void*>, int> caps;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = caps.find({dev, kern});
+    if (it == caps.end()) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            per_cu = cus = 0;
+        it = caps.emplace(std::make_pair(dev, kern), per_cu * cus).first;
+    }
+    return it->second;
+}
+
+// The whole perf-mode verify of stochastic target rows in ONE launch (k_stats<.., TAIL, SAMP>): the
+// spans, a decider and P.n_samp samplers per sequence, every workgroup resident (the decider and the
+// samplers poll).  1 launched, 0 not applicable (the caller runs k_stats + k_sample), < 0 an error.
+template <int DT>
+int32_t launch_fused_dt(const sd::Plan& P, bool fast, void* stream) {
+    const void* kern = fast ? (const void*)k_verify_fused<DT, true> : (const void*)k_verify_fused<DT, false>;
+    const int64_t head = (int64_t)P.B * (P.n_tslots * P.n_chunks + 1), total = head + (int64_t)P.B * P.n_samp;
+    // the spans and deciders resident at once with headroom (the deciders poll the spans); the
+    // samplers (after them in dispatch order) wait only for decisions and take freed slots
+    if (!poll_allowed() || 2 * head > resident_cap(kern)) return 0;
+    sd::Plan Q = P;
+    Q.kpoll = 1;
+    if (fast) SD_LAUNCH((k_verify_fused<DT, true>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+    else SD_LAUNCH((k_verify_fused<DT, false>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+    return 1;
+}
+
+int32_t launch_fused(const sd::Plan& P, void* stream) {
+    const bool fast = P.tT == 1.0f && P.dT == 1.0f && !P.t_keep && !P.d_keep;
+    if (P.tdt == SD_BF16) return launch_fused_dt<SD_BF16>(P, fast, stream);
+    if (P.tdt == SD_F16) return launch_fused_dt<SD_F16>(P, fast, stream);
+    return launch_fused_dt<SD_F32>(P, fast, stream);
 }
 
 int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, int slot_cnt, bool tail, void* stream) {
@@ -3524,6 +3817,32 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     if (!a->prof_stats_begin) {   // the batch-1 / few-sequence verify in one launch (sd_verify_lean.inc)
         const int32_t st = launch_verify_lean(P, stream);
         if (st) return st < 0 ? st : SD_OK;
+    }
+    // the verify in one launch (k_stats with a decider and samplers per sequence, fused_sampler): perf
+    // mode, stochastic target rows of one dtype, the drafter stats from the draws.  SD_FUSED=0 turns
+    // it off; by default it takes B >= 8 (fewer sequences: k_verify_lean above), SD_FUSED=2 any B.
+    if (perf && P.tails && !P.dec_in_sample && P.t_stoch && P.tdt == P.ddt && !P.draft_is_probs && P.dstats &&
+        P.stat_slots == P.n_tslots && P.n_tslots <= kFastSlots && P.n_chunks <= kWave && P.B <= kCntMax &&
+        !a->prof_stats_begin) {
+        int fmode = 1;
+        if (const char* e = getenv("SD_FUSED")) fmode = atoi(e);
+        if (fmode == 2 || (fmode == 1 && P.B >= 8)) {
+            Plan F = P;
+            F.rchunk = kThreads * kFusedEpt;
+            F.rn_chunks = (P.V + F.rchunk - 1) / F.rchunk;
+            F.n_samp = (F.rn_chunks + 1) / 2;   // two chunks per sampler (fused_sampler)
+            // records: the spans' (srec = rpart), the samplers' after them, the decisions after those
+            const size_t n_srec = (size_t)P.B * P.stat_slots * P.n_chunks;
+            const size_t need = n_srec + (size_t)P.B * F.rn_chunks + 2 * (size_t)P.B + 8;
+            const size_t have = (size_t)(P.B > a->batch * (2 * a->gamma + 1) ? P.B : a->batch * (2 * a->gamma + 1)) *
+                                (max_chunks(P.V) + 1) * sizeof(ResPart) / sizeof(uint4);
+            if (F.rn_chunks <= kTailChunks && need <= have) {
+                F.sprec = F.srec + n_srec;
+                F.drec = F.sprec + (size_t)P.B * F.rn_chunks;
+                const int32_t st = launch_fused(F, stream);
+                if (st) return st < 0 ? st : SD_OK;
+            }
+        }
     }
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
     const int reps = a->prof_stats_begin && a->prof_stats_repeat > 1 ? a->prof_stats_repeat : 1;
