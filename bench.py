@@ -313,12 +313,24 @@ def main():
                    "in_step_ms": (ms_per_step - verify_ms) / g,
                    "note": "ms: 20 graph-replayed launches over 8 rotating row sets; in_step_ms: the step's "
                            "draw phase / γ (kernel boundaries included)"},
-        "k_stats": {"ms": stats_ms, "launches_per_step": 1, "alg_bytes_per_launch": g * row_bytes},
-        "k_sample": {"ms": sample_ms, "launches_per_step": 1, "alg_bytes_per_launch": 2 * row_bytes,
-                     "note": "verify minus k_stats (graph-timed); rows re-read from L2 / Infinity Cache"},
     }
+    # sd_verify's dispatch (csrc/specdec_kernels.hip, sd_verify): Philox, stochastic rows, drafter stats
+    # from the draws and B >= 8 take the one-launch fused verify (k_verify_fused) unless SD_FUSED=0
+    fused = B >= 8 and os.environ.get("SD_FUSED", "1") != "0"
+    if fused:
+        kernels["k_verify_fused"] = {
+            "ms": verify_ms, "launches_per_step": 1, "alg_bytes_per_launch": (g + 1) * row_bytes,
+            "note": "the whole verify in one launch (graph-replayed verify steps); algorithmic bytes = the γ target "
+                    "rows once + the decided drafter row once (the decided target row is a re-read)"}
+        kernels["k_stats"] = {"ms": stats_ms, "launches_per_step": 0, "alg_bytes_per_launch": g * row_bytes,
+                              "note": "diagnostic: the two-launch path's statistics kernel (sd_verify's prof hook "
+                                      "runs it, not the fused launch), 20 back-to-back launches"}
+    else:
+        kernels["k_stats"] = {"ms": stats_ms, "launches_per_step": 1, "alg_bytes_per_launch": g * row_bytes}
+        kernels["k_sample"] = {"ms": sample_ms, "launches_per_step": 1, "alg_bytes_per_launch": 2 * row_bytes,
+                               "note": "verify minus k_stats (graph-timed); rows re-read from L2 / Infinity Cache"}
     for k in kernels.values():
-        k["ms_per_step"] = k["ms"] * k["launches_per_step"]
+        k["ms_per_step"] = k["ms"] * k["launches_per_step"]   # 0 for diagnostic entries
         k["achieved_gbs"] = k["alg_bytes_per_launch"] / (k["ms"] * 1e-3) / 1e9 if k["ms"] > 0 else None
         k["frac"] = k["achieved_gbs"] / HBM_PEAK_GBS if k["achieved_gbs"] else None
     dominant = max(kernels, key=lambda n: kernels[n]["ms_per_step"])
@@ -347,8 +359,8 @@ def main():
         shards = shard_lines(tl, dl, args, ops, _lib, PhiloxNoise, EngineStep)
 
     stream = None
-    if rank == 0 and args.stream_steps > 0:
-        stream = stream_line(tl, dl, row0, args, ops, _lib, StreamNoise)
+    if args.stream_steps > 0:   # every rank: batch-level data parallelism (bit-exact), weak scaling
+        stream = stream_line(tl, dl, row0, args, ops, _lib, StreamNoise, dp, dev, dist, world, rank)
     cfg1 = cfg4 = None
     if rank == 0 and world == 1 and not args.no_configs1:
         cfg1 = configs1_lines(dev, args, ops, _lib, PhiloxNoise)
@@ -426,33 +438,44 @@ def main():
         dist.destroy_process_group()
 
 
-def stream_line(tl, dl, row0, args, ops, _lib, StreamNoise):
+def stream_line(tl, dl, row0, args, ops, _lib, StreamNoise, dp, dev, dist, world, rank):
     """The same engine step in STREAM mode: the noise is the reference's own torch CPU generator
     stream (bit-exact tokens under torch.manual_seed), run as the drop-in engine runs it — inside
     a noise session (the generator state stays on the device) with one word reservation per step
     (StreamNoise.reserve: one jump-ahead + generation for the γ draws and the verify).  Eager
-    steps: the session's host bookkeeping sits between the calls."""
-    gen = torch.Generator().manual_seed(1234)
+    steps: the session's host bookkeeping sits between the calls.  With N ranks this is the
+    batch-level data parallelism of specdec_amd.engine.dp_runner (every rank decodes its own whole
+    batch of --batch rows from a generator seeded per batch, as engine/benchmark_executor.py:79
+    re-seeds; no exchange; exact per batch): weak scaling, 1 batch per rank; value = tokens of all
+    ranks / the slowest rank's time."""
+    gen = torch.Generator().manual_seed(1234 + rank)   # batch `rank`'s seed
     noise = StreamNoise(gen)
-    step = EngineStep(tl, dl, noise, row0, ops, _lib)
+    step = EngineStep(tl, dl, noise, 0, ops, _lib)     # a whole batch: rows 0..B-1 of its own
     B, g, V = step.B, step.g, step.V
     with noise.session():
         for _ in range(2):
             step()
         torch.cuda.synchronize()
         step.read_counts()
+        if dist:
+            dist.barrier()
         t0 = time.perf_counter()
         for _ in range(args.stream_steps):
             step()
         torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
         dt = time.perf_counter() - t0
         c = step.read_counts()
-    tokens = int(c[:, 1].sum())
     rsum, rcnt = positive_rate_sums(c[:, 0], g * args.stream_steps)
+    dt, tot = dp.aggregate(dt, {"tokens": int(c[:, 1].sum()), "rate_sum": rsum, "rate_cnt": rcnt}, dev, dist)
     ms = dt / args.stream_steps * 1e3
     words = g * 2 * B * V + B * (g + 2 * V)          # reserved per step (the verify's worst case)
-    return {"noise": "stream", "value": tokens / dt, "unit": "tokens/s", "ms_per_step": ms,
-            "steps": args.stream_steps, "rows": B, "acceptance_rate": rsum / rcnt if rcnt else 0.0,
+    return {"noise": "stream", "value": tot["tokens"] / dt, "unit": "tokens/s", "ms_per_step": ms,
+            "steps": args.stream_steps, "rows": B, "n_gpus": world, "batches_per_rank": 1,
+            "scaling": "weak", "exact": "bit-exact with the reference per batch (each rank's batch from its own "
+                                        "re-seeded torch generator: dp_runner's batch-level mode)",
+            "acceptance_rate": tot["rate_sum"] / tot["rate_cnt"] if tot["rate_cnt"] else 0.0,
             "logit_bytes_per_step": 2 * g * B * V * 2, "noise_words_per_step": words,
             "noise_bytes_per_step": words * 4 * 2,
             "note": "torch CPU generator words (bit-exact with the reference) made on the GPU, one reservation "
