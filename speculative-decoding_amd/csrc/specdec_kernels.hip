@@ -655,7 +655,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
 // The fused verify (stats_body with SAMP): grid = B x (spans + decider) then B x n_samp samplers (two
 // 2048-element chunks each)
 template <int DT, bool FAST>
-__global__ void __launch_bounds__(kThreads, 7) SD_SGPR_CAP k_verify_fused(Plan P, int slot_lo, int slot_cnt) {
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_verify_fused(Plan P, int slot_lo, int slot_cnt) {
     stats_body<DT, FAST, true, true>(P, slot_lo, slot_cnt);
 }
 
