@@ -55,7 +55,7 @@ def main():
     # (setup launches use others); bench.py reads "<family>_<workload_key>" for roofline.traffic
     pj = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     rec = json.load(open(pj)) if os.path.exists(pj) else {}
-    for fam in ("k_draw", "k_stats", "k_sample"):
+    for fam in ("k_draw", "k_stats", "k_sample", "k_verify_fused"):
         cands = sorted((k for k in acc if k.startswith(("sd::" + fam + "<", "sd::" + fam + "_lean<"))),
                        key=lambda k: -max(len(v) for v in acc[k].values()))
         if not cands:

@@ -2142,7 +2142,7 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
         uint4 r = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t tag = lane < 2 ? dec_tag(ep, b, lane) : 0u;
         for (int spin = 0;; ++spin) {
-            if (!have) {
+            if (!have && P.spin_limit >= 0) {   // < 0: the test hook, the decision counts as lost
                 r = ld_coh16(P.drec + 2 * b + lane);
                 have = r.w == tag;
             }

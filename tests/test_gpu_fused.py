@@ -89,7 +89,9 @@ def test_fused_verify_equals_two_launch_verify(B, V, rule, proc):
         b = run(tl, dl, rule, spec, seed, engine)
     for k in a:
         assert torch.equal(a[k].nan_to_num(), b[k].nan_to_num()), (k, a[k], b[k])
-    assert (a["row_status"] & 0x1).all()
+    active = (torch.arange(B) % 5 != 3) if engine else torch.ones(B, dtype=torch.bool)
+    assert (a["row_status"][active] & 0x1).all()          # every active row decided
+    assert not (a["row_status"][~active] & 0x1).any()     # inactive engine rows untouched (:250-258)
     assert not (a["row_status"] & 0x2C0).any()
 
 
