@@ -309,10 +309,11 @@ def main():
     row_bytes = B * V * 2
     kernels = {
         # per launch: algorithmic bytes = each logit row the kernel must read, once
-        "k_draw": {"ms": draw_ms, "launches_per_step": g, "alg_bytes_per_launch": row_bytes,
-                   "in_step_ms": (ms_per_step - verify_ms) / g,
-                   "note": "ms: 20 graph-replayed launches over 8 rotating row sets; in_step_ms: the step's "
-                           "draw phase / γ (kernel boundaries included)"},
+        "k_draw": {"ms": (ms_per_step - verify_ms) / g, "launches_per_step": g, "alg_bytes_per_launch": row_bytes,
+                   "isolated_ms": draw_ms,
+                   "note": "ms: the timed region's draw phase per launch = (step - the verify's graph-timed "
+                           "share) / γ; isolated_ms: 20 graph-replayed launches between HIP events, cycling over "
+                           "8 row sets (no L2-hot reuse); both include the dispatch gap between launches"},
     }
     # sd_verify's dispatch (csrc/specdec_kernels.hip, sd_verify): Philox, stochastic rows, drafter stats
     # from the draws and B >= 8 take the one-launch fused verify (k_verify_fused) unless SD_FUSED=0

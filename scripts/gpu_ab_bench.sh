@@ -20,7 +20,7 @@ for rep in $(seq $REPS); do
     envs="${c#*|}"
     echo -n "$label " >> gpurun_out/ab_bench.txt
     env $envs timeout -k 10 120 python bench.py --profile-only --steps 200 ${BENCH_ARGS} 2>>gpurun_out/ab_bench.err \
-      | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']; print(json.dumps({'ms_per_step': round(d['ms_per_step']*1e3,2), 'trials': [round(t*1e3,2) for t in d['replays']['trial_ms_per_step']], 'draw': round(k['k_draw']['ms']*1e3,2), 'draw_in_step': round(k['k_draw']['in_step_ms']*1e3,2), 'stats': round(k['k_stats']['ms']*1e3,2), 'sample': round(k['k_sample']['ms']*1e3,2), 'verify': round(d['phases_ms']['verify']*1e3,2)}))" \
+      | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernels']; print(json.dumps({'ms_per_step': round(d['ms_per_step']*1e3,2), 'trials': [round(t*1e3,2) for t in d['replays']['trial_ms_per_step']], 'draw_in_step': round(k['k_draw']['ms']*1e3,2), 'draw_isolated': round(k['k_draw']['isolated_ms']*1e3,2), 'verify': round(d['phases_ms']['verify']*1e3,2)}))" \
       >> gpurun_out/ab_bench.txt
   done
 done

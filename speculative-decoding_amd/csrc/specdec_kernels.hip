@@ -2119,6 +2119,9 @@ __global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
 //   A = {mode | slot << 8, mst.x, mst.y, tag}, B = {msd.x, msd.y, 0, tag}.
 // A sampler publishes its chunk record (sample_chunk) — or, for a sequence with nothing to sample,
 // an empty one — so the decider always waits for every sampler before it advances the epoch.
+#ifndef SD_SAMP_SLEEP
+#define SD_SAMP_SLEEP 2   // fused samplers' decision poll interval (s_sleep units of 64 clocks)
+#endif
 constexpr int kFusedEpt = 8;                       // k_sample's chunking: 2048-element chunks, the same draws
 
 __device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
@@ -2148,7 +2151,7 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
             }
             if (__all(have)) break;
             if (!spin_more(spin, P.spin_limit)) break;   // bounded: the finisher flags the row
-            __builtin_amdgcn_s_sleep(2);   // ~128 clocks: the decision is microseconds away
+            __builtin_amdgcn_s_sleep(SD_SAMP_SLEEP);   // the decision is microseconds away
         }
         if (lane < 2) s_rec[lane] = r;
         if (lane == 0) { s_ep = ep; s_ok = __all(have) ? 1 : 0; }
