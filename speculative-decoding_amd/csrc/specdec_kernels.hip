@@ -1035,7 +1035,8 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
 // The perf-mode walk (walk_core's rules) from two ballots over the drafts' accept and stop flags
 // (wave 0; lane 0 builds the Decision, carrying the sampled rows' (m, S) from lstat).
 __device__ __forceinline__ void walk_decision(const Plan& P, int b, const uint8_t* lacc, const uint8_t* lstop, bool act,
-                                              const float2* lstat, Decision* out, bool publish) {
+                                              const float2* lstat, Decision* out, bool publish,
+                                              int32_t extra_status = 0) {
     const int lane = threadIdx.x & 63;
     if (threadIdx.x < kWave) {
         const int g = P.gamma;
@@ -1080,6 +1081,7 @@ __device__ __forceinline__ void walk_decision(const Plan& P, int b, const uint8_
                 }
             }
         }
+        if (d.status & SD_ROW_DONE) d.status |= extra_status;   // e.g. a span record that never arrived
         if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision
             d.mst = lstat[d.slot];
             d.msd = d.mode == kModeResid && !P.draft_is_probs ? lstat[P.n_tslots + d.slot] : make_float2(0.f, 1.f);
@@ -1114,6 +1116,7 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
         }
         constexpr int kMaxSlotsPerWave = (kFastSlots + 3) / 4;
         float2 v[kMaxSlotsPerWave];
+        bool lost = false;   // a span record that never arrived: the row's outputs are invalid
         if (poll_epoch) {   // poll mode: each record re-read until it carries this call's tag (bounded)
             static_assert(kMaxSlotsPerWave <= 5, "ld_coh16x5");
             const uint32_t ep = *poll_epoch;
@@ -1142,6 +1145,7 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
                     }
                     v[k] = rr.z == tag ? make_float2(__uint_as_float(rr.x), __uint_as_float(rr.y))
                                        : make_float2(0.f, NAN);   // timeout: the row is flagged invalid
+                    lost |= rr.z != tag;
                 }
             }
             SD_TS(wg_id, 11);
@@ -1172,9 +1176,17 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
                 lacc[i] = accept_draft(P, p, q, pf.u);
             }
         }
+        __shared__ int32_t s_lost[kThreads / kWave];
+        if (lane == 0) s_lost[w] = __ballot(lost) != 0;
         __syncthreads();
         SD_TS(wg_id, 4);
         SD_TS(wg_id, 5);
+        int32_t xs = 0;
+#pragma unroll
+        for (int k = 0; k < kThreads / kWave; ++k) xs |= s_lost[k];
+        walk_decision(P, b, lacc, lstop, pf.act, lstat, out, publish,
+                      xs ? SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST : 0);
+        return;
     } else {
         seq_stats(P, b, lstat, publish);   // every wave reduces partials
         __syncthreads();
