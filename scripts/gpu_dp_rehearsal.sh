@@ -7,4 +7,4 @@ cd $GRAFT_REPO_ROOT
 SD_POLL=0 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 5 --dist-backend gloo --stream-steps 3 \
   > gpurun_out/dp2.json 2> gpurun_out/dp2.err
-python -c "import json; d=json.load(open('gpurun_out/dp2.json')); print({k: d[k] for k in ('value','n_gpus','ms_per_step')}); print(d['strong_scaling']); print({k: d['stream'][k] for k in ('value','n_gpus','ms_per_step','exact')})"
+python -c "import json; d=json.loads(open('gpurun_out/dp2.json').read().strip().splitlines()[-1]); print({k: d[k] for k in ('value','n_gpus','ms_per_step')}); print(d['strong_scaling']); print({k: d['stream'][k] for k in ('value','n_gpus','ms_per_step','exact')})"
