@@ -90,14 +90,17 @@ for rep in range(4):
     if (blk[head:, 0] > 0).any() and not LEAN:
         t0 = blk[blk[:, 0] > 0, 0].min()
         d = (blk - t0) / 100.0
+        d[:, 12:] = np.nan   # shader-clock columns
         d[blk == 0] = np.nan
         wgi = np.arange(8192)
         item = (wgi >> 3) % (nsp + 1)
         roles = {"span": (wgi < head) & (item < nsp), "decider": (wgi < head) & (item == nsp),
-                 "sampler": (wgi >= head) & (blk[:, 0] > 0)}
+                 "sampler": (wgi >= head) & (wgi < 4096) & (blk[:, 0] > 0),
+                 "finish": (wgi >= 4096) & (blk[:, 6] > 0)}
         names = {"span": {0: "start", 6: "stream_done", 1: "merged", 8: "rec_stored"},
-                 "decider": {0: "start", 7: "pf_done", 9: "polled", 11: "tags_ok", 3: "decided", 4: "tail_S",
-                             6: "finalized"},
+                 "decider": {0: "start", 7: "pf_done", 9: "polled", 11: "tags_ok", 10: "ratios", 4: "synced",
+                             5: "walked", 3: "decided"},
+                 "finish": {4: "tail_S", 7: "chunk_picked", 5: "candidate", 6: "finalized"},
                  "sampler": {0: "start", 1: "saw_decision", 8: "weights", 9: "chunk_pick", 2: "done"}}
         print("fused verify roles:")
         for r, m in roles.items():

@@ -1179,14 +1179,15 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
         }
         __shared__ int32_t s_lost[kThreads / kWave];
         if (lane == 0) s_lost[w] = __ballot(lost) != 0;
+        SD_TS(wg_id, 10);
         __syncthreads();
         SD_TS(wg_id, 4);
-        SD_TS(wg_id, 5);
         int32_t xs = 0;
 #pragma unroll
         for (int k = 0; k < kThreads / kWave; ++k) xs |= s_lost[k];
         walk_decision(P, b, lacc, lstop, pf.act, lstat, out, publish,
                       xs ? SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST : 0);
+        SD_TS(wg_id, 5);
         return;
     } else {
         seq_stats(P, b, lstat, publish);   // every wave reduces partials
@@ -2152,6 +2153,9 @@ __global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
 #ifndef SD_SAMP_SLEEP
 #define SD_SAMP_SLEEP 1   // fused samplers' decision poll interval (s_sleep units of 64 clocks)
 #endif
+#ifndef SD_SAMP_BOTH
+#define SD_SAMP_BOTH 1    // both chunks' loads issued before the first chunk's weights (-1.0 us at B=32)
+#endif
 constexpr int kFusedEpt = 8;                       // k_sample's chunking: 2048-element chunks, the same draws
 
 __device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
@@ -2243,6 +2247,28 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     // and scans) so they land meanwhile; only the weights of one chunk and the raw vectors of the
     // other are live together
     float wv[kFusedEpt], psum;
+#if SD_SAMP_BOTH
+    if constexpr (NV == 1) {
+        uint4 rt1 = make_uint4(0u, 0u, 0u, 0u), rd1 = rt1;
+        issue(c0);
+        if (has1) {
+            const int64_t e1 = (int64_t)c1 * P.rchunk + (int64_t)threadIdx.x * VEC;
+            rt1 = ld16_clamped<DT>(R.trow, e1, lastv);
+            if (R.resid) rd1 = ld16_clamped<DT>(R.drow, e1, lastv);
+        }
+        weights(c0, wv, psum);
+        SD_TS(wg_id, 8);
+        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id);
+        if (has1) {
+            rt[0] = rt1;
+            rd[0] = rd1;
+            weights(c1, wv, psum);
+            sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id);
+        }
+        SD_TS(wg_id, 2);
+        return;
+    }
+#endif
     issue(c0);
     weights(c0, wv, psum);
     if (NV == 1 && has1) issue(c1);   // fp32 rows (two vectors per chunk): after the draw, no spills
@@ -2282,7 +2308,8 @@ __device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decisio
     }
     __shared__ uint32_t s_ep2;
     if (threadIdx.x == 0) s_ep2 = epoch;
-    sample_finish<DT, DT, FAST, true, kFusedEpt>(P, d, b, R, u_row, wg_id, &s_ep2);
+    // (phase timestamps: the finish's on a row of its own, 4096 + wg)
+    sample_finish<DT, DT, FAST, true, kFusedEpt>(P, d, b, R, u_row, wg_id + 4096, &s_ep2);
 }
 
 // ------------------------------------------------------------------ sd_sample kernels
