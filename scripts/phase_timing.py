@@ -90,7 +90,6 @@ for rep in range(4):
     if (blk[head:, 0] > 0).any() and not LEAN:
         t0 = blk[blk[:, 0] > 0, 0].min()
         d = (blk - t0) / 100.0
-        d[:, 12:] = np.nan   # shader-clock columns
         d[blk == 0] = np.nan
         wgi = np.arange(8192)
         item = (wgi >> 3) % (nsp + 1)
@@ -98,7 +97,7 @@ for rep in range(4):
                  "sampler": (wgi >= head) & (wgi < 4096) & (blk[:, 0] > 0),
                  "finish": (wgi >= 4096) & (blk[:, 6] > 0)}
         names = {"span": {0: "start", 6: "stream_done", 1: "merged", 8: "rec_stored"},
-                 "decider": {0: "start", 7: "pf_done", 9: "polled", 11: "tags_ok", 10: "ratios", 4: "synced",
+                 "decider": {0: "start", 7: "pf_done", 9: "polled", 11: "tags_ok", 13: "reduced", 14: "ratio0", 15: "accept0", 10: "ratios", 4: "synced",
                              5: "walked", 3: "decided"},
                  "finish": {4: "tail_S", 7: "chunk_picked", 5: "candidate", 6: "finalized"},
                  "sampler": {0: "start", 1: "saw_decision", 8: "weights", 9: "chunk_pick", 2: "done"}}

@@ -459,6 +459,12 @@ __device__ __forceinline__ double wave_incl_scan_d(double v) {
     v += dpp_d<kDppRowBcast31, 0xC>(0.0, v);
     return v;
 }
+// a wave-uniform double into scalar registers (no VGPRs held across a long wait)
+__device__ __forceinline__ double uniform_d(double v) {
+    const uint64_t u = __double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u), hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 __device__ __forceinline__ double lane_d(double v, int lane) {
     const uint64_t x = __double_as_longlong(v);
     const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, lane);

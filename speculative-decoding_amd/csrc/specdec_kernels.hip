@@ -146,8 +146,8 @@ struct Plan {
     do {                                                                                       \
         if (threadIdx.x == 0 && P.ts) {                                                        \
             P.ts[(size_t)(wg) * 16 + (ph)] = __builtin_amdgcn_s_memrealtime();                 \
-            if ((ph) == 4 || (ph) == 10) P.ts[(size_t)(wg) * 16 + 12 + ((ph) == 10)] = __builtin_amdgcn_s_memtime(); \
-            if ((ph) == 1 || (ph) == 2) P.ts[(size_t)(wg) * 16 + 14 + ((ph) == 2)] = __builtin_amdgcn_s_memtime(); \
+            if ((wg) >= 8192 && ((ph) == 4 || (ph) == 10)) P.ts[(size_t)(wg) * 16 + 12 + ((ph) == 10)] = __builtin_amdgcn_s_memtime(); \
+            if ((wg) >= 8192 && ((ph) == 1 || (ph) == 2)) P.ts[(size_t)(wg) * 16 + 14 + ((ph) == 2)] = __builtin_amdgcn_s_memtime(); \
         }                                                                                      \
     } while (0)
 #else
@@ -456,10 +456,11 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
         SD_TS(wg_id, 7);
         if constexpr (SAMP) {
             __shared__ Decision s_dec;
+            const double u_row = uniform_d(cdf_uniform(P.noise, (uint32_t)b));   // the chunk pick's, ahead of the records
             decide_seq(P, b, pf, wg_id, &s_dec, true, true, &s_epoch);
             __syncthreads();
             SD_TS(wg_id, 3);
-            fused_finish<DT, FAST>(P, b, s_dec, s_epoch, wg_id);
+            fused_finish<DT, FAST>(P, b, s_dec, s_epoch, wg_id, u_row);
         } else {
             decide_seq(P, b, pf, wg_id, nullptr, true, true, &s_epoch);
             SD_TS(wg_id, 3);
@@ -1169,12 +1170,15 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
                 lstat[s] = ms;
                 if (publish) P.rowstat[b * P.slots + s] = ms;
             }
+            if (k == 0) SD_TS(wg_id, 13);
             if (lane == k && i == s) {   // i < γ: this thread holds draft s
                 float p, q;
                 draft_ratio(P, b, i, pf, ms, pf.ds, p, q);
+                if (k == 0 && s == 0) SD_TS(wg_id, 14);
                 lp[i] = p;
                 lq[i] = q;
                 lacc[i] = accept_draft(P, p, q, pf.u);
+                if (k == 0 && s == 0) SD_TS(wg_id, 15);
             }
         }
         __shared__ int32_t s_lost[kThreads / kWave];
@@ -2023,8 +2027,7 @@ __device__ __forceinline__ Decision load_decision(const Plan& P, int b) {
 // chunk c's draw from weights already in registers (sample_chunk's second half)
 template <int TDT, int DDT, int EPT>
 __device__ __forceinline__ void sample_chunk_pick(const Plan& P, int b, int c, const float* wv, float psum, uint32_t tag,
-                                                  int wg_id) {
-    const double u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
+                                                  int wg_id, double u) {
     const int64_t base = (int64_t)c * P.rchunk;
     double T;
     float PT;
@@ -2041,8 +2044,11 @@ __device__ __forceinline__ void sample_chunk_pick(const Plan& P, int b, int c, c
 }
 
 template <int TDT, int DDT, bool FAST, int EPT = 8>
-__device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, int b, int c, uint32_t tag, int wg_id = 0) {
+__device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, int b, int c, uint32_t tag, int wg_id = 0,
+                                             double u = -1.0) {
     constexpr int VEC = PairVec<TDT, DDT>::kVec, NV = EPT / VEC;
+    // the chunk's uniform (its Philox offset may be a device load) before the rows' loads
+    if (u < 0.0) u = cdf_uniform(P.noise, (uint32_t)b, 1u + (uint32_t)c);
     float psum = 0.f;
     const int64_t base = (int64_t)c * P.rchunk;
     float wv[EPT];
@@ -2054,7 +2060,7 @@ __device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, i
         for (int k = 0; k < VEC; ++k) psum += pv[k];
     }
     SD_TS(wg_id, 8);
-    sample_chunk_pick<TDT, DDT, EPT>(P, b, c, wv, psum, tag, wg_id);
+    sample_chunk_pick<TDT, DDT, EPT>(P, b, c, wv, psum, tag, wg_id, u);
 }
 
 // grid (chunk, B).  STOCH: chunk Σ weight; greedy (!STOCH): the exact argmax-candidate bodies.
@@ -2153,9 +2159,6 @@ __global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
 #ifndef SD_SAMP_SLEEP
 #define SD_SAMP_SLEEP 1   // fused samplers' decision poll interval (s_sleep units of 64 clocks)
 #endif
-#ifndef SD_SAMP_BOTH
-#define SD_SAMP_BOTH 1    // both chunks' loads issued before the first chunk's weights (-1.0 us at B=32)
-#endif
 constexpr int kFusedEpt = 8;                       // k_sample's chunking: 2048-element chunks, the same draws
 
 __device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
@@ -2164,12 +2167,56 @@ __device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
     return h | 1u;
 }
 
+// pair_weights_from's FAST weights of one 16-bit vector pair (T = 1, no processor, drafter logits),
+// the same values and psum order, with the row's mode (RESID) and the chunk's raggedness (WHOLE:
+// every element inside the vocabulary) out of the element loop
+template <int DT, bool RESID, bool WHOLE>
+__device__ __forceinline__ void fused_weights_v(const PairRows& R, int64_t e0, uint4 rt, uint4 rd, float* w, float& psum) {
+    constexpr int VEC = Elem<DT>::kVec;
+    float xt[VEC], xd[VEC];
+    if (WHOLE) unpack16<DT>(rt, xt);
+    else finish16<DT>(rt, R.trow, e0, R.V, xt);
+    if (RESID) {
+        if (WHOLE) unpack16<DT>(rd, xd);
+        else finish16<DT>(rd, R.drow, e0, R.V, xd);
+    }
+    psum = 0.f;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+        float p = prob_fast<DT>(xt[k], R.mst.x, R.t_inv);
+        float v = p;
+        if (RESID) {
+            const float diff = p - prob_fast<DT>(xd[k], R.msd.x, R.d_inv);
+            v = diff > 0.f ? diff : 0.f;
+        }
+        if (!WHOLE && !(e0 + k < R.V)) v = p = 0.f;
+        w[k] = v;
+        psum += p;
+    }
+}
+template <int DT>
+__device__ __forceinline__ void fused_weights(const PairRows& R, int cc, int rchunk, int64_t e0, uint4 rt, uint4 rd,
+                                              float* w, float& psum) {
+    const bool whole = (int64_t)(cc + 1) * rchunk <= R.V;
+    if (R.resid) {
+        if (whole) fused_weights_v<DT, true, true>(R, e0, rt, rd, w, psum);
+        else fused_weights_v<DT, true, false>(R, e0, rt, rd, w, psum);
+    } else {
+        if (whole) fused_weights_v<DT, false, true>(R, e0, rt, rd, w, psum);
+        else fused_weights_v<DT, false, false>(R, e0, rt, rd, w, psum);
+    }
+}
+
 template <int DT, bool FAST>
 __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int wg_id) {
     __shared__ uint4 s_rec[2];
     __shared__ uint32_t s_ep;
     __shared__ int32_t s_ok;
     SD_TS(wg_id, 0);
+    // the two chunks' in-chunk uniforms depend on (b, c) only: computed (and the Philox offset, a
+    // device load under graph replays, fetched) while the decision is still being made
+    const double u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)c));
+    const double u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)c));
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
         uint32_t ep = 0;
@@ -2216,11 +2263,34 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     const int c0 = 2 * c, c1 = 2 * c + 1;
     const bool has1 = c1 < P.rn_chunks;
     if (!(R.t_al && (!R.resid || R.d_al) && P.V >= VEC)) {   // misaligned rows: one chunk at a time
-        sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c0, sample_tag(ep, b, c0), wg_id);
-        if (has1) sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c1, sample_tag(ep, b, c1), wg_id);
+        sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c0, sample_tag(ep, b, c0), wg_id, u0);
+        if (has1) sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c1, sample_tag(ep, b, c1), wg_id, u1);
         return;
     }
     const int64_t lastv = last_whole_vec<DT>(P.V);
+    float wv[kFusedEpt], psum;
+    if constexpr (NV == 1 && FAST) {
+        // 16-bit rows (one vector per thread and chunk): both chunks' vectors in flight at once, then
+        // each chunk's weights (the sampled row's mode and the chunk's raggedness hoisted out of the
+        // element loop) and draw
+        const int64_t e0 = (int64_t)c0 * P.rchunk + (int64_t)threadIdx.x * VEC, e1 = e0 + P.rchunk;
+        const uint4 t0 = ld16_clamped<DT>(R.trow, e0, lastv);
+        const uint4 d0 = R.resid ? ld16_clamped<DT>(R.drow, e0, lastv) : make_uint4(0u, 0u, 0u, 0u);
+        uint4 t1 = make_uint4(0u, 0u, 0u, 0u), d1 = t1;
+        if (has1) {
+            t1 = ld16_clamped<DT>(R.trow, e1, lastv);
+            if (R.resid) d1 = ld16_clamped<DT>(R.drow, e1, lastv);
+        }
+        fused_weights<DT>(R, c0, P.rchunk, e0, t0, d0, wv, psum);
+        SD_TS(wg_id, 8);
+        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id, u0);
+        if (has1) {
+            fused_weights<DT>(R, c1, P.rchunk, e1, t1, d1, wv, psum);
+            sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
+        }
+        SD_TS(wg_id, 2);
+        return;
+    }
     uint4 rt[NV], rd[NV];
     auto issue = [&](int cc) {
 #pragma unroll
@@ -2243,41 +2313,17 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
             for (int k = 0; k < VEC; ++k) psum += pv[k];
         }
     };
-    // chunk c0's vectors, its weights, then chunk c1's loads go out before c0's draw (its barriers
-    // and scans) so they land meanwhile; only the weights of one chunk and the raw vectors of the
-    // other are live together
-    float wv[kFusedEpt], psum;
-#if SD_SAMP_BOTH
-    if constexpr (NV == 1) {
-        uint4 rt1 = make_uint4(0u, 0u, 0u, 0u), rd1 = rt1;
-        issue(c0);
-        if (has1) {
-            const int64_t e1 = (int64_t)c1 * P.rchunk + (int64_t)threadIdx.x * VEC;
-            rt1 = ld16_clamped<DT>(R.trow, e1, lastv);
-            if (R.resid) rd1 = ld16_clamped<DT>(R.drow, e1, lastv);
-        }
-        weights(c0, wv, psum);
-        SD_TS(wg_id, 8);
-        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id);
-        if (has1) {
-            rt[0] = rt1;
-            rd[0] = rd1;
-            weights(c1, wv, psum);
-            sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id);
-        }
-        SD_TS(wg_id, 2);
-        return;
-    }
-#endif
+    // the general rows (fp32, processors): chunk c0's vectors, its weights, then chunk c1's loads go
+    // out before c0's draw; only the weights of one chunk and the raw vectors of the other are live
     issue(c0);
     weights(c0, wv, psum);
     if (NV == 1 && has1) issue(c1);   // fp32 rows (two vectors per chunk): after the draw, no spills
     SD_TS(wg_id, 8);
-    sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id);
+    sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id, u0);
     if (has1) {
         if (NV != 1) issue(c1);
         weights(c1, wv, psum);
-        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id);
+        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
     }
     SD_TS(wg_id, 2);
 }
@@ -2286,7 +2332,8 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
 // chunk records (always every one of them, so none is left polling an advanced epoch) and the
 // token / outputs as k_sample's tail writes them.
 template <int DT, bool FAST>
-__device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decision& d0, uint32_t epoch, int wg_id) {
+__device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decision& d0, uint32_t epoch, int wg_id,
+                                             double u_row) {
     Decision d = d0;
     if (d.mode < kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) d.mode = kModeNone;
     if (threadIdx.x == 0) {
@@ -2294,7 +2341,6 @@ __device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decisio
         st_coh16(P.drec + 2 * b, make_uint4(mslot, __float_as_uint(d.mst.x), __float_as_uint(d.mst.y), dec_tag(epoch, b, 0)));
         st_coh16(P.drec + 2 * b + 1, make_uint4(__float_as_uint(d.msd.x), __float_as_uint(d.msd.y), 0u, dec_tag(epoch, b, 1)));
     }
-    const double u_row = cdf_uniform(P.noise, (uint32_t)b);   // the chunk pick's uniform, before the wait
     PairRows R{};
     if (d.mode != kModeNone) R = pair_rows<DT, DT>(P, d, b);
     if (d.mode == kModeNone) {
