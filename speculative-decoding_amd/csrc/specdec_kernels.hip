@@ -2181,17 +2181,49 @@ __device__ __forceinline__ void fused_weights_v(const PairRows& R, int64_t e0, u
         else finish16<DT>(rd, R.drow, e0, R.V, xd);
     }
     psum = 0.f;
+    if constexpr (DT == SD_BF16) {
+        // pairs on packed fp32 (v_pk_add / v_pk_mul: the same IEEE operations as prob_fast's, two
+        // lanes per instruction) and one v_cvt_pk_bf16_f32 per pair
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        typedef __bf16 h2 __attribute__((ext_vector_type(2)));
+        constexpr float kL2e = 1.44269502162933349609375f;
+        auto prob2 = [](f2 y, float m, float inv) {
+            f2 e = (y - m) * kL2e;
+            e.x = __builtin_amdgcn_exp2f(e.x);
+            e.y = __builtin_amdgcn_exp2f(e.y);
+            return __builtin_convertvector(__builtin_convertvector(e * inv, h2), f2);
+        };
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) {
-        float p = prob_fast<DT>(xt[k], R.mst.x, R.t_inv);
-        float v = p;
-        if (RESID) {
-            const float diff = p - prob_fast<DT>(xd[k], R.msd.x, R.d_inv);
-            v = diff > 0.f ? diff : 0.f;
+        for (int k = 0; k < VEC; k += 2) {
+            f2 p = prob2(f2{xt[k], xt[k + 1]}, R.mst.x, R.t_inv);
+            f2 v = p;
+            if (RESID) {
+                const f2 diff = p - prob2(f2{xd[k], xd[k + 1]}, R.msd.x, R.d_inv);
+                v.x = diff.x > 0.f ? diff.x : 0.f;
+                v.y = diff.y > 0.f ? diff.y : 0.f;
+            }
+            if (!WHOLE) {
+                if (!(e0 + k < R.V)) v.x = p.x = 0.f;
+                if (!(e0 + k + 1 < R.V)) v.y = p.y = 0.f;
+            }
+            w[k] = v.x;
+            w[k + 1] = v.y;
+            psum += p.x;
+            psum += p.y;
         }
-        if (!WHOLE && !(e0 + k < R.V)) v = p = 0.f;
-        w[k] = v;
-        psum += p;
+    } else {
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+            float p = prob_fast<DT>(xt[k], R.mst.x, R.t_inv);
+            float v = p;
+            if (RESID) {
+                const float diff = p - prob_fast<DT>(xd[k], R.msd.x, R.d_inv);
+                v = diff > 0.f ? diff : 0.f;
+            }
+            if (!WHOLE && !(e0 + k < R.V)) v = p = 0.f;
+            w[k] = v;
+            psum += p;
+        }
     }
 }
 template <int DT>
