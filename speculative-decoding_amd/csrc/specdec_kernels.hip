@@ -336,6 +336,7 @@ __device__ __forceinline__ void pf_late(const Plan& P, int b, int i, DraftPf& pf
     bool ovr = false;
     pf.u = draw_uniform(P, b, i, 0, &ovr);   // perf mode: Philox, no stream words
 }
+template <int DT = -1, bool FAST = false>
 __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out = nullptr,
                            bool publish = true, bool coh = true, const uint32_t* poll_epoch = nullptr);
 
@@ -457,7 +458,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
         if constexpr (SAMP) {
             __shared__ Decision s_dec;
             const double u_row = uniform_d(cdf_uniform(P.noise, (uint32_t)b));   // the chunk pick's, ahead of the records
-            decide_seq(P, b, pf, wg_id, &s_dec, true, true, &s_epoch);
+            decide_seq<DT, FAST>(P, b, pf, wg_id, &s_dec, true, true, &s_epoch);
             __syncthreads();
             SD_TS(wg_id, 3);
             fused_finish<DT, FAST>(P, b, s_dec, s_epoch, wg_id, u_row);
@@ -1011,11 +1012,17 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
 }
 
 // p(x_i), q(x_i) of draft i from its prefetch and the rows' (m, S)
+template <int DT = -1, bool FAST = false>
 __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const DraftPf& pf, float2 mst, float2 msd,
                                             float& p, float& q) {
     p = 0.f;
     q = 0.f;
     if (pf.tok < 0 || pf.tok >= P.V) return;
+    if constexpr (DT >= 0 && FAST) {   // both rows of dtype DT, unprocessed, drafter logits
+        p = round_dt<DT>(sd_exp(pf.xt - mst.x) / mst.y);
+        q = round_dt<DT>(sd_exp(pf.xd - msd.x) / msd.y);
+        return;
+    }
     const int rt = b * P.slots + i;
     const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const float yt = P.tdt == SD_BF16 ? process_value<SD_BF16>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
@@ -1103,6 +1110,10 @@ __device__ __forceinline__ void walk_decision(const Plan& P, int b, const uint8_
 // uniforms, the walk.  Every per-draft input was prefetched during the stream (DraftPf), so the
 // tail has one memory round trip (the partials).  With the drafter stats prefetched (P.dstats)
 // the wave that reduces target slot i tests draft i at once: one barrier before the walk.
+// DT >= 0 (the fused verify's decider): rows of that dtype, FAST rows unprocessed, the drafter
+// stats from the draws and the one-round-trip record path guaranteed by the launch — only that
+// path is compiled (a shorter, branch-free critical path after the records)
+template <int DT, bool FAST>
 __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& pf, int wg_id, Decision* out, bool publish, bool coh,
                            const uint32_t* poll_epoch) {
     __shared__ float2 lstat[2 * SD_MAX_GAMMA + 1];
@@ -1111,7 +1122,7 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = kThreads / kWave;
     const int i = pf_draft(P);
     if (i >= 0) lstop[i] = pf.stop;
-    if (P.dstats && P.n_chunks <= kWave && P.n_tslots <= kFastSlots) {
+    if (DT >= 0 || (P.dstats && P.n_chunks <= kWave && P.n_tslots <= kFastSlots)) {
         if (i >= 0) {
             lstat[P.n_tslots + i] = pf.ds;
             if (publish) P.rowstat[b * P.slots + P.n_tslots + i] = pf.ds;
@@ -1173,7 +1184,7 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
             if (k == 0) SD_TS(wg_id, 13);
             if (lane == k && i == s) {   // i < γ: this thread holds draft s
                 float p, q;
-                draft_ratio(P, b, i, pf, ms, pf.ds, p, q);
+                draft_ratio<DT, FAST>(P, b, i, pf, ms, pf.ds, p, q);
                 if (k == 0 && s == 0) SD_TS(wg_id, 14);
                 lp[i] = p;
                 lq[i] = q;
