@@ -12,7 +12,8 @@ residual samples from.  Independent prompt batches shard data-parallel (one repl
 no collective on the data path), so scaling is weak: every rank verifies its own 32 rows.
 
 value = output tokens (accepted drafts + resampled tokens, all ranks, counted exactly by the
-verify kernel itself: sd_verify_args.row_counts) / max-over-ranks wall time of the K timed steps.
+verify kernel itself: sd_verify_args.row_counts) / max-over-ranks wall time of the K timed steps,
+per trial; the median of the trials' ratios is reported.
 Steps run as hipGraph replays — G = --graph-steps steps (default 20) per captured graph, K/G replays per
 timed trial; --trials trials of exactly K steps (median reported), each replay also timed by HIP events —
 and noise is in-kernel Philox (perf mode).
@@ -73,6 +74,8 @@ def parse():
     ap.add_argument("--profile-only", action="store_true",
                     help="only the B-row engine step (no shards, configs[1]/[4], STREAM or CPU lines): every "
                          "sd:: launch of the run has the headline shape, for rocprofv3 / PMC passes")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="dispatch option for A/B runs (sd_set_option), e.g. FUSED_VERIFY=0 or LEAN_VERIFY=0")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsing N ranks on fewer GPUs)")
     a = ap.parse_args()
@@ -242,6 +245,9 @@ def main():
     from specdec_amd import _lib, dp, ops
     from specdec_amd.noise import PhiloxNoise, StreamNoise
 
+    for kv in args.option:   # A/B runs: another kernel path for the same outputs
+        k, v = kv.split("=", 1)
+        _lib.set_option(getattr(_lib, f"SD_OPT_{k.upper()}"), int(v))
     g, V = args.gamma, args.vocab
     # weak scaling (the value): args.batch rows per rank, the global batch split contiguously by row
     # (specdec_amd/dp.py); Philox noise is keyed by the global row id, so the shards draw what one GPU
@@ -255,19 +261,28 @@ def main():
     for _ in range(max(args.warmup, 1)):
         step()
     torch.cuda.synchronize()
+    # which verify kernels the step runs, as the library reports it (sd_last_verify_path)
+    verify_path = _lib.last_verify_path()
     # the K timed steps: one captured graph of G steps (G = --graph-steps, dividing K), replayed K/G times
     # per trial; --trials trials of exactly K steps, each bracketed by a barrier and a device sync, the
     # median trial reported (every trial's tokens counted exactly by the verify kernel)
     graph, outs, replays = graph_steps(step, args.steps, args.graph_steps, noise, g + 1)
     G = len(outs)
     step.read_counts()                                   # drop the warm-up / capture replay's counts
-    replay_ms, trial_s = [], []
+    replay_ms, trial_s, trial_rate, trial_tok = [], [], [], []
+    acc_t = torch.zeros(B, dtype=torch.long)
     for _ in range(max(args.trials, 1)):
-        trial_s.append(timed_replays(graph, replays, dist, replay_ms))
-    elapsed = statistics.median(trial_s)
-    counts = step.read_counts()                          # exact: every timed step's tokens
+        t = timed_replays(graph, replays, dist, replay_ms)
+        c = step.read_counts()                           # exact: this trial's tokens (outside the timed region)
+        acc_t += c[:, 0]
+        t, tt = dp.aggregate(t, {"tokens": int(c[:, 1].sum())}, dev, dist)
+        trial_s.append(t)
+        trial_tok.append(tt["tokens"])
+        trial_rate.append(tt["tokens"] / t)
     n_trials = len(trial_s)
-    tokens_t, acc_t = int(counts[:, 1].sum()) / n_trials, counts[:, 0]
+    mid = sorted(range(n_trials), key=lambda i: trial_rate[i])[n_trials // 2]   # the median trial
+    value = trial_rate[mid]
+    elapsed = trial_s[mid]
     rsum_t, rcnt_t = positive_rate_sums(acc_t, g * args.steps * n_trials)
 
     # acceptance over a larger untimed sample (>= 200 steps of the same graph, fresh noise each)
@@ -281,7 +296,7 @@ def main():
     vgraph, _, vrep = graph_steps(step.verify, args.steps, args.graph_steps)
     verify_ms = statistics.median(timed_replays(vgraph, vrep, None) for _ in range(3)) / args.steps * 1e3
 
-    elapsed, tot = dp.aggregate(elapsed, {"tokens": tokens_t, "accepted": float(acc_t.sum()),
+    _, tot = dp.aggregate(elapsed, {"accepted": float(acc_t.sum()),
                                           "drafted": B * g * args.steps * n_trials, "rate_sum": rsum, "rate_cnt": rcnt,
                                           "rate_sum_t": rsum_t, "rate_cnt_t": rcnt_t,
                                           "accepted_c": float(counts_c[:, 0].sum()),
@@ -315,10 +330,8 @@ def main():
                            "share) / γ; isolated_ms: 20 graph-replayed launches between HIP events, cycling over "
                            "8 row sets (no L2-hot reuse); both include the dispatch gap between launches"},
     }
-    # sd_verify's dispatch (csrc/specdec_kernels.hip, sd_verify): Philox, stochastic rows, drafter stats
-    # from the draws and B >= 8 take the one-launch fused verify (k_verify_fused) unless SD_FUSED=0
-    fused = B >= 8 and os.environ.get("SD_FUSED", "1") != "0"
-    if fused:
+    # sd_verify's dispatch as the library reported it for the step's verify (sd_last_verify_path)
+    if verify_path == _lib.SD_PATH_VERIFY_FUSED:
         kernels["k_verify_fused"] = {
             "ms": verify_ms, "launches_per_step": 1, "alg_bytes_per_launch": (g + 1) * row_bytes,
             "note": "the whole verify in one launch (graph-replayed verify steps); algorithmic bytes = the γ target "
@@ -326,6 +339,9 @@ def main():
         kernels["k_stats"] = {"ms": stats_ms, "launches_per_step": 0, "alg_bytes_per_launch": g * row_bytes,
                               "note": "diagnostic: the two-launch path's statistics kernel (sd_verify's prof hook "
                                       "runs it, not the fused launch), 20 back-to-back launches"}
+    elif verify_path == _lib.SD_PATH_VERIFY_LEAN:
+        kernels["k_verify_lean"] = {"ms": verify_ms, "launches_per_step": 1, "alg_bytes_per_launch": g * row_bytes,
+                                    "note": "the whole verify in one launch (graph-replayed verify steps)"}
     else:
         kernels["k_stats"] = {"ms": stats_ms, "launches_per_step": 1, "alg_bytes_per_launch": g * row_bytes}
         kernels["k_sample"] = {"ms": sample_ms, "launches_per_step": 1, "alg_bytes_per_launch": 2 * row_bytes,
@@ -387,7 +403,7 @@ def main():
         step_gbs = step_bytes / (ms_per_step * 1e-3) / 1e9
         line = {
             "metric": METRIC,
-            "value": tot["tokens"] / elapsed,
+            "value": value,
             "unit": "tokens/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -402,21 +418,23 @@ def main():
                                    "γ drafter draws + verify (rule A10)",
                        "rows_per_gpu": args.batch, "global_batch": args.batch * world, "gamma": g, "vocab": V,
                        "parallelism": f"dp{world}", "noise": "philox", "graph_steps": G, "replays_per_trial": replays,
-                       "trials": n_trials},
+                       "trials": n_trials, "verify_path": _lib.PATH_NAMES.get(verify_path, str(verify_path))},
             # engine/metrics.py:123-129: mean of per-row acc/tot over the rows with a positive rate,
             # over >= 200 untimed steps of the same graph (the timed steps' own figure beside it)
             "acceptance_rate": tot["rate_sum"] / tot["rate_cnt"] if tot["rate_cnt"] else 0.0,
             "acceptance_rate_pooled": tot["accepted_c"] / tot["drafted_c"],
             "acceptance_steps": G * n_count,
             "acceptance_rate_timed": tot["rate_sum_t"] / tot["rate_cnt_t"] if tot["rate_cnt_t"] else 0.0,
-            "tokens_timed": tot["tokens"],
+            "tokens_timed": trial_tok[mid],
             "replays": {"count": replays * n_trials, "steps_per_replay": G,
                         "ms_median": statistics.median(replay_ms), "ms_min": min(replay_ms),
                         "ms_max": max(replay_ms),
                         "ms_per_step_median": statistics.median(replay_ms) / G,
                         "trial_ms_per_step": [t / args.steps * 1e3 for t in trial_s],
+                        "trial_tokens_per_s": trial_rate,
                         "note": "HIP events between back-to-back replays of the captured steps (rank 0); "
-                                "trial_ms_per_step: each trial's wall time / K (the value uses the median)"},
+                                "trial_ms_per_step: each trial's wall time / K; value = the median trial's "
+                                "tokens / its time (ms_per_step is that trial's)"},
             "roofline": {"bound": "hbm", "achieved": dk["achieved_gbs"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": dk["frac"], "traffic": traffic,
                          "kernel": dominant, "kernel_ms": dk["ms"], "launches_per_step": dk["launches_per_step"],
@@ -509,13 +527,25 @@ def shard_lines(tl, dl, args, ops, _lib, PhiloxNoise, EngineStep):
 
 
 def configs4_line(dev, args, ops, _lib, PhiloxNoise):
-    """configs[4]: the n-gram-assisted verify step (ngram_assisted/ngram_assisted.py:104-141, rule
-    A11) — γ=8, top-p 0.9, filler top-3 over 9 synthetic Llama-3 shaped target rows (batch 1),
-    drafts the target agrees with; hipGraph replays, Philox noise."""
+    """configs[4]: the n-gram-assisted verify step (ngram_assisted/ngram_assisted.py:111-164, rule
+    A11) — γ=8, top-p 0.9, filler top-3 over 9 synthetic Llama-3 shaped target rows (batch 1);
+    hipGraph replays, Philox noise.
+
+    What is drafted: A11 accepts draft i iff a draw from the processed target row i equals it
+    (sample-and-compare), so its accept rate is p_i(draft_i).  An LM's next-token rows are peaked (the
+    loop goldens' token-Markov banks are, tests/fakelm.py); here every target row is N(0, 1) noise
+    with ONE hot token at logit 12.9 + U(0, 1.5), whose probability after the top-p 0.9 cut is
+    ~0.6-0.85, and the draft at each position is that hot token (an n-gram store that predicts the
+    row's likeliest continuation).  So the timed steps run the accept walk over several positions,
+    the filler over the accepted ones and the final draw — not the reject-at-0 path alone."""
     g, V = 8, args.vocab
     gen = torch.Generator(device=dev).manual_seed(21)
-    tl = (torch.randn(1, g + 1, V, generator=gen, device=dev) * 3.0).to(torch.bfloat16)
-    draft = tl[0, :g].float().argmax(-1).unsqueeze(0).contiguous()
+    x = torch.randn(1, g + 1, V, generator=gen, device=dev)
+    hot = torch.randint(0, V, (1, g + 1), generator=gen, device=dev)
+    boost = 12.9 + 1.5 * torch.rand(1, g + 1, generator=gen, device=dev)
+    x.scatter_(2, hot.unsqueeze(-1), boost.unsqueeze(-1))
+    tl = x.to(torch.bfloat16)
+    draft = hot[:, :g].contiguous()
     stops = torch.tensor([128001, 128009], dtype=torch.long, device=dev)
     proc = ops.ProcSpec("nucleus", 1.0, 0, 0.9)
     noise = PhiloxNoise(seed=9, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
@@ -529,11 +559,18 @@ def configs4_line(dev, args, ops, _lib, PhiloxNoise):
     torch.cuda.synchronize()
     graph, outs, replays = graph_steps(step, 200, 20, noise, 1)
     dt = timed_replays(graph, replays, None)
-    n = torch.stack([o.n_accepted.long() for o in outs]).sum().item()
     steps = len(outs) * replays
-    return {"us_per_step": dt / steps * 1e6, "tokens_per_s": (n + len(outs)) * replays / dt,
-            "accepted_per_step": n / len(outs), "alg_bytes_per_step": (g + 1) * V * 2,
-            "gamma": g, "top_p": 0.9, "filler_top_k": 3, "rule": "A11"}
+    # the acceptance over 50 more replays (fresh Philox noise each): the captured outputs hold the
+    # last replay's values, so read them after every replay
+    acc = []
+    for _ in range(50):
+        graph.replay()
+        acc.append(torch.stack([o.n_accepted.long() for o in outs]).sum())
+    n = float(torch.stack(acc).sum().item()) / (50 * len(outs))
+    return {"us_per_step": dt / steps * 1e6, "tokens_per_s": (n + 1) * steps / dt,
+            "accepted_per_step": n, "alg_bytes_per_step": (g + 1) * V * 2,
+            "gamma": g, "top_p": 0.9, "filler_top_k": 3, "rule": "A11",
+            "drafts": "the hot token of each peaked target row (p after the top-p cut ~0.6-0.85)"}
 
 
 def configs1_lines(dev, args, ops, _lib, PhiloxNoise):

@@ -35,8 +35,9 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 9
-#define SD_MAX_GAMMA 32
+#define SD_ABI_VERSION 10
+#define SD_MAX_GAMMA 32          /* drafts per call; specdec_amd.ops chunks longer windows */
+#define SD_NGRAM_MAX_FILLER 64   /* sd_ngram_verify filler_k                                    */
 
 typedef enum {
     SD_OK = 0,
@@ -272,6 +273,40 @@ int32_t sd_set_poll_policy(int32_t allow_poll, int32_t spin_limit);
 int32_t sd_get_poll_policy(int32_t* allow_poll, int32_t* spin_limit);
 const char* sd_last_hip_error(void);   /* hipGetErrorString of the last failed launch (this thread) */
 
+/* Dispatch options (ABI 10): switches between kernel paths that compute the same outputs, for
+ * A/B runs and for tests that compare the paths.  Process-wide, set by the caller; no entry point
+ * reads the environment (SD_POLL / SD_POLL_SPIN_LIMIT seed the poll policy once, at first use).
+ * sd_set_option returns SD_ERR_INVALID for an unknown option or value.                        */
+typedef enum {
+    SD_OPT_FUSED_VERIFY = 1,    /* 1 (default): k_verify_fused for B >= 8; 2: any B; 0: never    */
+    SD_OPT_LEAN_VERIFY = 2,     /* -1 (default): k_verify_lean for <= 8 sequences; 1: any batch
+                                   the occupancy check admits; 0: never                           */
+    SD_OPT_THRESHOLD_POLL = 3,  /* 1 (default): the top-k / nucleus search in one launch when its
+                                   grid is resident; 0: the launch-per-phase design               */
+    SD_OPT_DRAW_STREAM = 4,     /* 1 (default): STREAM multinomial draws in one pass
+                                   (k_draw_stream); 0: statistics + race + finalize launches      */
+} sd_option;
+int32_t sd_set_option(int32_t option, int32_t value);
+int32_t sd_get_option(int32_t option, int32_t* value);
+
+/* The kernel path the CALLING THREAD's last successful sd_verify / sd_sample took (so a test or a
+ * bench can tell which kernel it measured without reading the dispatch rules).                 */
+typedef enum {
+    SD_PATH_NONE = 0,
+    SD_PATH_VERIFY_LEAN = 1,        /* k_verify_lean: one launch, <= 8 sequences                 */
+    SD_PATH_VERIFY_FUSED = 2,       /* k_verify_fused: one launch                                 */
+    SD_PATH_VERIFY_TWO_LAUNCH = 3,  /* k_stats (+ decider) then k_sample                          */
+    SD_PATH_VERIFY_STREAM = 4,      /* STREAM: k_stats, k_decide, k_walk, k_resample, k_finalize  */
+    SD_PATH_SAMPLE_DRAW_LEAN = 16,  /* k_draw_lean (PHILOX multinomial, T = 1, 16-bit)           */
+    SD_PATH_SAMPLE_DRAW = 17,       /* k_draw (PHILOX, processors / fp32)                          */
+    SD_PATH_SAMPLE_NUCLEUS = 18,    /* k_draw_nuc (PHILOX nucleus by rejection)                    */
+    SD_PATH_SAMPLE_STREAM = 19,     /* k_draw_stream (STREAM one pass)                             */
+    SD_PATH_SAMPLE_GREEDY_LEAN = 20,/* k_draw_lean<GREEDY>                                          */
+    SD_PATH_SAMPLE_MULTI = 21,      /* row statistics + k_rowsample + k_sample_finalize            */
+} sd_path;
+int32_t sd_last_verify_path(void);
+int32_t sd_last_sample_path(void);
+
 /* Workspaces: device memory of at least sd_*_workspace_size bytes, ZERO-FILLED ONCE when
  * allocated (hipMemset).  Its first block holds per-sequence arrival counters that the PHILOX
  * verify path uses to run each sequence's decision / sampling in the last workgroup to finish;
@@ -308,7 +343,7 @@ typedef struct {
     sd_processor proc;           /* the loop's logits_processor                                */
     const int64_t* stop_tokens;
     int32_t n_stop;
-    int32_t filler_k;            /* 0..8                                                       */
+    int32_t filler_k;            /* 0..SD_NGRAM_MAX_FILLER                                     */
     sd_noise noise;
     /* outputs, device */
     int32_t* n_accepted;         /* [B] n                                                      */

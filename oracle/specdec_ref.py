@@ -157,6 +157,19 @@ def max_fn(x: torch.Tensor) -> torch.Tensor:
 # --------------------------------------------------------------------------
 # verify step, batch-1 rule (sampling/speculative_decoding.py:129-171)
 # --------------------------------------------------------------------------
+def stop_location(accepted: Sequence[int], stops: Sequence[int]) -> int:
+    """Where the loops return on a stop token among the accepted drafts, or -1
+    (sampling/speculative_decoding.py:150-152, ngram_assisted/ngram_assisted.py:124-126):
+    ``torch.nonzero(torch.eq(drafts[1, n], stop_tokens[S, 1]))[0, 1]`` — the [S, n] comparison is
+    scanned row-major, so the stop token LISTED FIRST that occurs wins, at its first position (not
+    the earliest stop position when several listed stops occur)."""
+    acc = [int(t) for t in accepted]
+    for s in stops:
+        if int(s) in acc:
+            return acc.index(int(s))
+    return -1
+
+
 @dataclass
 class SpecStep:
     n: int                      # accepted drafts
@@ -264,9 +277,9 @@ def speculative_generate(inputs: List[int], drafter, target, gamma: int = 5,
         r = noise.uniform(g)                                       # :139
         n, p = spec_accept(rows, q, ids[0, cur:cur + g].tolist(), proc, r, exact)
         accepted += n                                              # :147
-        hit = [j for j in range(n) if int(ids[0, cur + j]) in stops]   # :150-155
-        if hit:
-            return ids[0, plen:cur + hit[0] + 1].tolist(), accepted / speculated
+        hit = stop_location(ids[0, cur:cur + n].tolist(), stops)    # :150-155
+        if hit >= 0:
+            return ids[0, plen:cur + hit + 1].tolist(), accepted / speculated
         # the final multinomial's Exp noise (:171) comes after r; its dtype only changes rounding
         E = noise.exponential((V,)) if proc.stochastic else None
         step = spec_resample(rows, q, p, n, proc, E, skip_sample_adjustment, exact)
@@ -506,9 +519,9 @@ def ngram_assisted_generate(inputs: List[int], store: NgramStore, target, gamma:
                 n = i
                 break
         acc += n
-        for j in range(n):                                               # :126-131
-            if drafted[cur + j] in stops:
-                return drafted[P:cur + j + 1], rate()
+        hit = stop_location(drafted[cur:cur + n], stops)                 # :124-129
+        if hit >= 0:
+            return drafted[P:cur + hit + 1], rate()
         p_p = process(logits[cur + g - 1:cur + g], proc, exact)[0] if n == g else p[n]   # :134-143
         x = int(sample(p_p, proc, noise).reshape(-1)[0])
         ids[cur:cur + n] = drafted[cur:cur + n]

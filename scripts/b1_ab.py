@@ -1,8 +1,8 @@
 """configs[1] batch-1 step times (bench.configs1_lines: γ=4 draws + verify, hipGraph replays) under
-environment A/B settings read at capture time (GPU box):
+dispatch-option A/B settings (sd_set_option, applied at capture time; GPU box):
 
-    python scripts/b1_ab.py "SD_STATS_STAGES=8" "SD_STATS_STAGES=1" ...
-Each argument is a space-separated list of VAR=value pairs ("" = defaults); prints one JSON line each.
+    python scripts/b1_ab.py "" "LEAN_VERIFY=0" ...
+Each argument is a space-separated list of OPTION=value pairs ("" = defaults); prints one JSON line each.
 """
 import json
 import os
@@ -24,16 +24,14 @@ for spec in sys.argv[1:] or [""]:
     saved = {}
     for kv in spec.split():
         k, v = kv.split("=", 1)
-        saved[k] = os.environ.get(k)
-        os.environ[k] = v
+        o = getattr(_lib, f"SD_OPT_{k.upper()}")
+        saved[o] = _lib.get_option(o)
+        _lib.set_option(o, int(v))
     res = {}
     for rep in range(2):
         r = bench.configs1_lines(dev, args, ops, _lib, PhiloxNoise)
         for name, d in r.items():
             res.setdefault(name, []).append(round(d["us_per_step"], 2))
     print(json.dumps({"env": spec, "us_per_step": res}), flush=True)
-    for k, v in saved.items():
-        if v is None:
-            os.environ.pop(k, None)
-        else:
-            os.environ[k] = v
+    for o, v in saved.items():
+        _lib.set_option(o, v)

@@ -1,9 +1,8 @@
 """Which kernels the batch-1 (configs[1]) verify takes per processor: runs one bench-shaped step
-with SD_LEAN_DEBUG=1 (launch_verify_lean reports "launched" / "not applicable (k)")."""
+and prints the library's own report (sd_last_verify_path / sd_last_sample_path)."""
 import os
 import sys
 
-os.environ["SD_LEAN_DEBUG"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "speculative-decoding_amd")]
 import torch  # noqa: E402
@@ -22,7 +21,8 @@ for name, proc in (("multinomial", ops.ProcSpec("multinomial", 1.0)), ("nucleus"
     dstats = torch.empty(g, 1, 2, dtype=torch.float32, device=dev) if not proc.keeps else None
     for d in range(g):
         ops.sample_rows(dl[:, d], proc, noise, tokens_out=draft[:, d], row_stats_out=dstats[d] if dstats is not None else None)
-    print(f"--- {name}: verify", file=sys.stderr, flush=True)
+    draw = _lib.PATH_NAMES.get(_lib.last_sample_path())
     ops.verify([tl[:, t] for t in range(g + 1)], [dl[:, t] for t in range(g)], draft, _lib.SD_RULE_SPEC, proc, proc,
                noise, torch.tensor([128001], device=dev), draft_row_stats=dstats)
     torch.cuda.synchronize()
+    print(f"{name}: draws {draw}, verify {_lib.PATH_NAMES.get(_lib.last_verify_path())}", flush=True)

@@ -4,8 +4,8 @@ Loads the SD_PHASE_TIMING build (make -C speculative-decoding_amd timing) and dr
 128256 bf16 (T = 1, Philox) — the bench's drafter draw — and prints, for the producer spans and
 for the rows' last spans (the pollers), when they reach each phase, µs after the launch's first
 start (s_memrealtime, 100 MHz).  Phases: 0 start, 1 loads landed (wave max), 2 span pick done,
-3 record stored (producers), 4 poll done (last spans), 5 outputs written.  SD_DRAW_AFFINE=1 places
-a row's spans on one XCD group (read once per process).
+3 record stored (producers), 4 poll done (last spans), 5 outputs written.
+(An XCD-affine placement of a row's spans was measured slower and removed in round 5.)
 """
 import os
 import sys

@@ -21,7 +21,7 @@ from specdec_amd.noise import PhiloxNoise  # noqa: E402
 B, G, V = int(os.environ.get("B", 32)), 4, 128256
 SPEC = os.environ.get("RULE", "engine") == "spec"
 NT = G + 1 if SPEC else G
-LEAN = os.environ.get("SD_LEAN_VERIFY", "1") != "0" and B <= 8
+LEAN = B <= 8   # the default dispatch (SD_OPT_LEAN_VERIFY = -1): k_verify_lean for <= 8 sequences
 dev = torch.device("cuda")
 g = torch.Generator(device=dev).manual_seed(0)
 tl = (torch.randn(B, NT, V, device=dev, generator=g) * 3).to(torch.bfloat16)

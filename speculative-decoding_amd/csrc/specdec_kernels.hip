@@ -121,12 +121,9 @@ struct Plan {
     struct ThrRow* thr;   //   per-row tie request
     uint32_t* cnt;        // per-sequence arrival counters (seq_counter): set 0 k_stats, set 1 k_sample
     uint64_t* ts;         // SD_PHASE_TIMING builds only: per-workgroup phase timestamps
-    int32_t tails;        // perf mode: decide / finish in last-arrival tails (1) or own launches (0)
-    int32_t dec_in_sample;   // perf mode, stochastic rows: the decision is computed in k_sample (DEC)
     int32_t coh;          // partials may come from the same launch: read them agent-coherently
     int32_t xcd_affine;   // B % 8 == 0: all workgroups of sequence b share XCD group b % 8
-    int32_t stats_interleave;   // k_stats: workgroup c of a row takes stages c, c + n_chunks, ...
-    int32_t spoll;        // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
+    int32_t spoll;       // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
     int32_t kpoll;        // k_stats (decide tail): poll-mode partials (tagged records, no counter)
     int32_t thr_poll;     // k_thr_hist: slice maxima exchanged in-launch (no k_thr_max launch)
     int32_t spin_limit;   // poll modes: re-reads before a record counts as lost (sd_set_poll_policy)
@@ -194,6 +191,28 @@ __device__ __forceinline__ bool is_stop(const Plan& P, int64_t tok) {
     for (int k = 0; k < P.n_stop; ++k)
         if (P.stops[k] == tok) return true;
     return false;
+}
+
+// The loops' stop scan over the accepted drafts (sampling/speculative_decoding.py:150-152,
+// ngram_assisted/ngram_assisted.py:124-126) is nonzero(eq(drafts[1, n], stop_tokens[S, 1]))[0, 1]:
+// row-major over [S, n], so the stop token LISTED FIRST that occurs wins, at its first position —
+// not the earliest stop position when several listed stops occur.  A draft's stop rank is its
+// token's first position in the list (INT_MAX: not a stop); the 8-bit form is rank + 1 (0: not a
+// stop), saturating at 255 — then the exact rank is recomputed from the list.
+__device__ __forceinline__ int stop_rank(const Plan& P, int64_t tok) {
+    for (int k = 0; k < P.n_stop; ++k)
+        if (P.stops[k] == tok) return k;
+    return INT_MAX;
+}
+__device__ __forceinline__ uint8_t stop_rank8(const Plan& P, int64_t tok) {
+    uint32_t r = 0;
+    for (int k = P.n_stop - 1; k >= 0; --k)   // no early exit: the last hit is the first occurrence
+        if (P.stops[k] == tok) r = k < 254 ? (uint32_t)k + 1u : 255u;
+    return (uint8_t)r;
+}
+// the rank of draft j from its 8-bit form (the list re-read only for saturated ranks)
+__device__ __forceinline__ int stop_rank_of(const Plan& P, uint8_t r8, int64_t tok) {
+    return r8 == 0 ? INT_MAX : r8 < 255 ? (int)r8 - 1 : stop_rank(P, tok);
 }
 
 // stop list staged in LDS by a tail (nullptr / too many stops: the global list)
@@ -310,7 +329,7 @@ struct DraftPf {
     int64_t tok = -1;
     float xt = 0.f, xd = 0.f, u = 0.f;
     float2 ds = make_float2(-INFINITY, 0.f);
-    bool stop = false;
+    uint8_t stop = 0;   // stop_rank8 of the drafted token
     bool act = true;   // engine rule: the sequence is active (draft 0's thread only)
 };
 __device__ __forceinline__ int pf_draft(const Plan& P) {
@@ -328,10 +347,7 @@ __device__ __forceinline__ void pf_late(const Plan& P, int b, int i, DraftPf& pf
     if (i < 0) return;
     fetch_drafted(P, b, i, pf.tok, &pf.xt, &pf.xd);
     if (P.dstats) pf.ds = P.dstats[(int64_t)i * P.dstats_stride + b];
-    bool st = false;
-#pragma unroll 4
-    for (int k = 0; k < P.n_stop; ++k) st |= P.stops[k] == pf.tok;   // no early exit
-    pf.stop = st;
+    pf.stop = stop_rank8(P, pf.tok);
     if (i == 0 && P.active) pf.act = P.active[b] != 0;
     bool ovr = false;
     pf.u = draw_uniform(P, b, i, 0, &ovr);   // perf mode: Philox, no stream words
@@ -495,14 +511,11 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     const float T = is_t ? P.tT : P.dT;
     const bool has_keep = !FAST && (is_t ? P.t_keep : P.d_keep);
     const RowKeep kp = has_keep ? keep_of(P, r) : RowKeep{-INFINITY, INT_MAX, 0, 0};
-    // This workgroup's stages (STEP elements each) of the row: interleaved (stage chunk + i * n_chunks,
-    // so concurrently running workgroups stream adjacent blocks) or one contiguous span.
+    // This workgroup's stages (STEP elements each) of the row: one contiguous span.
     const int nst = (P.V + STEP - 1) / STEP;
     const int spw = P.chunk / STEP;
-    const bool ilv = P.stats_interleave != 0;
-    const int cnt = ilv ? (chunk < nst ? (nst - chunk + P.n_chunks - 1) / P.n_chunks : 0)
-                        : (chunk * spw < nst ? min(spw, nst - chunk * spw) : 0);
-    auto stage_of = [&](int i) -> int64_t { return ilv ? chunk + (int64_t)i * P.n_chunks : (int64_t)chunk * spw + i; };
+    const int cnt = chunk * spw < nst ? min(spw, nst - chunk * spw) : 0;
+    auto stage_of = [&](int i) -> int64_t { return (int64_t)chunk * spw + i; };
     const int64_t hi = P.V;
     const bool aligned = (reinterpret_cast<uintptr_t>(row) & 15) == 0;
     // the row's last stage is partial when STEP does not divide V: it is this workgroup's last, if any
@@ -826,8 +839,13 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
         used = g;
         d.n = n;
         // :150-155 stop token among the accepted drafts -> the reference returns before sampling
-        for (int j = 0; j < n; ++j)
-            if (lstop ? lstop[j] != 0 : is_stop(P, P.draft_tokens[b * P.tok_stride + j])) { d.stop_index = j; break; }
+        // (the first-LISTED stop token that occurs, at its first position: stop_rank)
+        int best = INT_MAX;
+        for (int j = 0; j < n; ++j) {
+            const int r = lstop && lstop[j] < 255 ? (lstop[j] == 0 ? INT_MAX : (int)lstop[j] - 1)
+                                                  : stop_rank(P, P.draft_tokens[b * P.tok_stride + j]);
+            if (r < best) { best = r; d.stop_index = j; }
+        }
         if (d.stop_index >= 0) {
             d.mode = kModeNone;
             d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
@@ -952,7 +970,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                 lrq[i] = q;
                 // accept iff u <= p/q (fp32, SPEC) / u < min(1, p/q) (fp64, ENGINE): accept_draft's rules
                 lthr[i] = spec ? (double)(p / q) : ((double)q <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)q));
-                lstop[i] = is_stop(P, P.draft_tokens[b * P.tok_stride + d]) ? 1 : 0;
+                lstop[i] = stop_rank8(P, P.draft_tokens[b * P.tok_stride + d]);
                 lact[i] = P.active == nullptr || P.active[b] != 0;
             }
             __syncthreads();
@@ -1055,6 +1073,22 @@ __device__ __forceinline__ void walk_decision(const Plan& P, int b, const uint8_
         const int f_rej = rejm ? __builtin_ctzll(rejm) : g;             // first rejected draft (g: none)
         const uint64_t before = f_rej >= 64 ? ~0ull : ((1ull << f_rej) - 1ull);
         const uint64_t stop_acc = stopm & before;                        // stop tokens among the accepted
+        // SPEC: the first-LISTED stop token among the accepted drafts, at its first position (the
+        // reference's row-major nonzero, stop_rank); the ENGINE ends a row at its first accepted stop
+        int spec_stop = -1;
+        if (P.rule == SD_RULE_SPEC && stop_acc) {   // wave-uniform
+            const bool sa = ((stop_acc >> lane) & 1ull) != 0;
+            const int key = wave_min_i(sa ? ((int)lstop[lane] << 8) | lane : INT_MAX);
+            spec_stop = key & 0xff;
+            if ((key >> 8) == 255 && lane == 0) {   // saturated ranks (> 253 stop tokens): exact
+                int best = INT_MAX;
+                for (uint64_t m = stop_acc; m; m &= m - 1) {
+                    const int j = __builtin_ctzll(m);
+                    const int r = stop_rank(P, P.draft_tokens[b * P.tok_stride + j]);
+                    if (r < best) { best = r; spec_stop = j; }
+                }
+            }
+        }
         if (lane != 0) return;
         Decision d{};
         d.stop_index = -1;
@@ -1062,7 +1096,7 @@ __device__ __forceinline__ void walk_decision(const Plan& P, int b, const uint8_
         if (P.rule == SD_RULE_SPEC) {
             d.n = f_rej;
             if (stop_acc) {
-                d.stop_index = __builtin_ctzll(stop_acc);
+                d.stop_index = spec_stop;
                 d.mode = kModeNone;
                 d.status = SD_ROW_DONE | SD_ROW_STOP_IN_DRAFTS;
             } else {
@@ -1219,16 +1253,6 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
         SD_TS(wg_id, 5);
     }
     walk_decision(P, b, lacc, lstop, pf.act, lstat, out, publish);
-}
-
-// grid (B): decide_seq as its own launch (perf mode without the k_stats tail)
-__global__ void __launch_bounds__(kThreads) k_decide_perf(Plan P) {
-    const int b = blockIdx.x;
-    DraftPf pf;
-    const int i = pf_draft(P);
-    pf_early(P, b, i, pf);
-    pf_late(P, b, i, pf);
-    decide_seq(P, b, pf, 8192 - 1 - b);
 }
 
 // STREAM exponential race of one chunk: the exact argmax (first index on ties) of
@@ -2075,40 +2099,23 @@ __device__ __forceinline__ void sample_chunk(const Plan& P, const PairRows& R, i
 }
 
 // grid (chunk, B).  STOCH: chunk Σ weight; greedy (!STOCH): the exact argmax-candidate bodies.
-// TAIL: the last workgroup of each sequence runs sample_finish; otherwise k_sample_finish does.
-// DEC (stochastic rows): no k_stats tail ran; every workgroup of sequence b computes the decision
-// itself from the row-statistics partials (decide_seq: one round trip for the partials and the
-// drafted ids, one for the drafted logits) and chunk 0 publishes it.  The decision then costs the
-// sampler ~1 round trip instead of a three-round-trip tail (store, counter, reload) at the end of
-// the streaming kernel.
-template <int TDT, int DDT, bool FAST, bool STOCH, bool TAIL, bool DEC = false>
+// The last workgroup of each sequence (poll mode: its last chunk) runs sample_finish.  (A variant
+// that moved the decision into every sampling workgroup measured 63.9 vs 61.9 us per step and was
+// removed in round 5, with the own-launch decide / finish kernels.)
+template <int TDT, int DDT, bool FAST, bool STOCH>
 __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     constexpr int EPT = 8;
+    constexpr bool TAIL = true;
     const int wg_id = 8192 + blockIdx.y * gridDim.x + blockIdx.x;
     int b, c;
     if (P.xcd_affine) affine_split(wg_id - 8192, (int)gridDim.x, b, c);
     else { b = blockIdx.y; c = blockIdx.x; }
     SD_TS(wg_id, 0);
-    Decision d;
-    if constexpr (DEC) {
-        __shared__ Decision s_dec;
-        DraftPf pf;
-        const int pi = pf_draft(P);
-        pf_early(P, b, pi, pf);
-        pf_late(P, b, pi, pf);
-        // partials of the previous launch: plain, cacheable loads (every workgroup of the sequence
-        // reads the same lines: coherent loads would each go to memory)
-        decide_seq(P, b, pf, wg_id, &s_dec, c == 0, false);
-        __syncthreads();
-        d = s_dec;
-        if (d.mode < kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) d.mode = kModeNone;
-    } else {
-        d = load_decision(P, b);
-    }
+    const Decision d = load_decision(P, b);
     // the tail's chunk-pick uniform, computed while the decision load is in flight
-    const double u_row = STOCH && TAIL ? cdf_uniform(P.noise, (uint32_t)b) : 0.0;
+    const double u_row = STOCH ? cdf_uniform(P.noise, (uint32_t)b) : 0.0;
     // poll mode (stochastic tails): this call's epoch of sequence b, read beside the decision load
-    const bool poll = STOCH && TAIL && !DEC && P.spoll;
+    const bool poll = STOCH && P.spoll;
     uint32_t epoch = 0;
     if (poll) epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     PairRows R{};
@@ -2147,18 +2154,6 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
         if (!s_last) return;
         sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, u_row, wg_id);
     }
-}
-
-// grid (B): sample_finish as its own launch (no arrival counters)
-template <int TDT, int DDT, bool FAST, bool STOCH>
-__global__ void __launch_bounds__(kThreads) k_sample_finish(Plan P) {
-    const int b = blockIdx.x;
-    SD_TS(16384 - 1 - b, 0);
-    const Decision d = load_decision(P, b);
-    PairRows R{};
-    if (STOCH && d.mode != kModeNone) R = pair_rows<TDT, DDT>(P, d, b);
-    SD_TS(16384 - 1 - b, 1);
-    sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, STOCH ? cdf_uniform(P.noise, (uint32_t)b) : 0.0, 16384 - 1 - b);
 }
 
 // ------------------------------------------------------------------ fused verify (k_stats<.., SAMP>)
@@ -2290,12 +2285,17 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     d.mst = make_float2(__uint_as_float(A.y), __uint_as_float(A.z));
     d.msd = make_float2(__uint_as_float(Bq.x), __uint_as_float(Bq.y));
     const bool ok = s_ok != 0;
-    if (!ok || d.mode <= kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) {
-        // nothing to draw (or the decision was lost): empty records for both chunks
+    // The decision never came: publish NOTHING.  The epoch this sampler read may already be the next
+    // call's (it was dispatched after its decider gave up waiting and advanced it), and a record
+    // tagged with it would pass the next call's check; the decider's own bounded wait flags the row
+    // (SD_ROW_EXCHANGE_TIMEOUT) without it.
+    if (!ok) return;
+    if (d.mode <= kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) {
+        // nothing to draw: empty records for both chunks (the decider waits for every sampler)
         if (threadIdx.x < 2 && 2 * c + (int)threadIdx.x < P.rn_chunks) {
             const int cc = 2 * c + (int)threadIdx.x;
             st_coh16(reinterpret_cast<float4*>(P.sprec) + (int64_t)b * P.rn_chunks + cc,
-                     make_uint4(0u, 0u, (uint32_t)(ok ? -1 : kLostDecision), sample_tag(ep, b, cc)));
+                     make_uint4(0u, 0u, (uint32_t)-1, sample_tag(ep, b, cc)));
         }
         return;
     }
@@ -2782,7 +2782,6 @@ struct DrawLean {
     int32_t poll;      // 1: the row's last span polls tagged partials (no arrival counter)
     int32_t spin_limit;   // bounded poll (sd_set_poll_policy)
     int32_t* status_or;   // the caller's sticky error word (nullable)
-    int32_t affine;       // rows % 8 == 0: every span of a row on one XCD group (affine_split)
     uint64_t* ts;         // phase timestamps (SD_PHASE_TIMING builds only)
 };
 
@@ -2853,8 +2852,8 @@ __device__ int greedy_rescan(const DrawLean& A, const char* row, int c, float M,
 template <int DT, int NST, bool GREEDY = false>
 __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     constexpr int VEC = 8, STEP = kThreads * VEC, EPT = NST * VEC, NW = kThreads / kWave;
-    int c = blockIdx.x, r = blockIdx.y;
-    if (A.affine) affine_split(blockIdx.y * gridDim.x + blockIdx.x, (int)gridDim.x, r, c);
+    // (XCD-affine placement of a row's spans measured slower, 6.6 vs 6.4 us: plain grid order)
+    const int c = blockIdx.x, r = blockIdx.y;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int ts_wg = r * A.n_span + c;
     SD_TSL(ts_wg, 0);
@@ -3243,6 +3242,8 @@ constexpr int kDefaultSpin = 1 << 16;
 std::atomic<int> g_allow_poll{-1};
 std::atomic<int> g_spin_limit{kDefaultSpin};
 std::once_flag g_policy_once;
+// The only environment reads of the library: the poll policy's initial values, once per process
+// (the DP runner's shared-device rehearsal sets SD_POLL=0 before the first call).
 void policy_init() {
     std::call_once(g_policy_once, [] {
         int allow = 1;
@@ -3255,6 +3256,23 @@ void policy_init() {
         }
     });
 }
+
+// Dispatch options (sd_set_option), indexed by sd_option; relaxed reads on every call.
+std::atomic<int> g_opt_fused{1}, g_opt_lean{-1}, g_opt_thr_poll{1}, g_opt_draw_stream{1};
+std::atomic<int>* option_slot(int32_t opt) {
+    switch (opt) {
+        case SD_OPT_FUSED_VERIFY: return &g_opt_fused;
+        case SD_OPT_LEAN_VERIFY: return &g_opt_lean;
+        case SD_OPT_THRESHOLD_POLL: return &g_opt_thr_poll;
+        case SD_OPT_DRAW_STREAM: return &g_opt_draw_stream;
+        default: return nullptr;
+    }
+}
+inline int opt(const std::atomic<int>& o) { return o.load(std::memory_order_relaxed); }
+
+// the path of this thread's last sd_verify / sd_sample (sd_last_*_path)
+thread_local int32_t g_verify_path = SD_PATH_NONE;
+thread_local int32_t g_sample_path = SD_PATH_NONE;
 bool poll_allowed() {
     policy_init();
     return g_allow_poll.load(std::memory_order_relaxed) > 0;
@@ -3328,19 +3346,16 @@ bool needs_keep(const sd_processor& p) { return p.kind >= SD_PROC_TOPK; }
 // workgroups (2 per CU), all resident at once.  Measured at the bench shape (128 rows of 128256
 // bf16): 512 workgroups 13.6 us, 1024 14.4, 2048 16.3, 384 14.7, 256 15.9 — longer spans mean
 // fewer arrivals and partials per sequence for the decision tail, until the stream itself thins
-// out.  SD_STATS_STAGES overrides (tuning).
+// out.  Contiguous spans (interleaved stages measured 39.2 vs 38.4 us per step, removed).
 // Other callers (sd_sample's greedy / STREAM statistics, A11) keep target_wgs = 2048.
 void set_stats_chunks(sd::Plan& P, int rows, int target_wgs = 2048, int min_stages = 1) {
     const int64_t stage = kThreads * 8;
     const int64_t stages_per_row = (P.V + stage - 1) / stage;
     int64_t per_wg = (rows * stages_per_row + target_wgs - 1) / target_wgs;
     per_wg = per_wg < min_stages ? min_stages : per_wg;
-    if (const char* e = getenv("SD_STATS_STAGES")) per_wg = atoi(e);
     per_wg = per_wg < 1 ? 1 : (per_wg > 64 ? 64 : per_wg);
     P.chunk = (int32_t)(per_wg * stage);
     P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
-    P.stats_interleave = 0;   // measured: contiguous spans 38.4 us/step vs interleaved 39.2
-    if (const char* e = getenv("SD_STATS_INTERLEAVE")) P.stats_interleave = atoi(e);
 }
 
 // Resample / sample passes: 1 or 2 stages of 2048 elements per workgroup, about 1024 workgroups so
@@ -3372,8 +3387,7 @@ int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt,
     const dim3 grid(P.n_chunks, P.B * slot_cnt);
     // poll-mode decide tail: the drafter stats came with the draws (target slots only, one launch)
     sd::Plan Q = P;
-    static const bool kp_off = getenv("SD_STATS_POLL") && atoi(getenv("SD_STATS_POLL")) == 0;   // A/B
-    Q.kpoll = TAIL && !kp_off && P.dstats && P.n_chunks <= kWave && P.stat_slots == P.n_tslots &&
+    Q.kpoll = TAIL && P.dstats && P.n_chunks <= kWave && P.stat_slots == P.n_tslots &&
               P.n_tslots <= sd::kFastSlots && slot_lo == 0 &&
               slot_cnt == P.stat_slots &&
               sample_poll_ok(P.B, fast ? (const void*)k_stats<DT, true, TAIL> : (const void*)k_stats<DT, false, TAIL>);
@@ -3440,24 +3454,10 @@ int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, in
 
 // A poll-mode exchange (k_sample's finish, k_stats' decide tail) needs its B consumers plus producers
 // resident: 2B <= the kernel's resident capacity (occupancy x CUs, per device and kernel, queried
-// once); SD_SAMPLE_POLL=0 keeps the arrival counters (A/B)
+// once); sd_set_poll_policy(0, ·) keeps the arrival counters
 bool sample_poll_ok(int B, const void* kern) {
-    static const bool off = getenv("SD_SAMPLE_POLL") && atoi(getenv("SD_SAMPLE_POLL")) == 0;
-    if (off || !poll_allowed()) return false;
-    static std::mutex mu;
-    static std::map<std::pair<int, const void*>, int> caps;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return false;
-    std::lock_guard<std::mutex> lk(mu);
-    auto it = caps.find({dev, kern});
-    if (it == caps.end()) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            per_cu = cus = 0;
-        it = caps.emplace(std::make_pair(dev, kern), per_cu * cus).first;
-    }
-    return 2 * B <= it->second;
+    if (!poll_allowed()) return false;
+    return 2 * B <= resident_cap(kern);
 }
 
 template <int TDT, int DDT>
@@ -3468,42 +3468,16 @@ int32_t launch_resample_dd(const sd::Plan& P, void* stream) {
     if (P.noise.mode == SD_NOISE_STREAM) {
         if (fast) SD_LAUNCH((k_resample<TDT, DDT, 8, true>), grid, dim3(kThreads), stream, P);
         else SD_LAUNCH((k_resample<TDT, DDT, 8, false>), grid, dim3(kThreads), stream, P);
+    } else if (P.t_stoch) {
+        // poll-mode finish when the consumers (one per sequence) leave room for every producer
+        sd::Plan Q = P;
+        Q.spoll = sample_poll_ok(P.B, fast ? (const void*)k_sample<TDT, DDT, true, true>
+                                           : (const void*)k_sample<TDT, DDT, false, true>);
+        if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true>), grid, dim3(kThreads), stream, Q);
+        else SD_LAUNCH((k_sample<TDT, DDT, false, true>), grid, dim3(kThreads), stream, Q);
     } else {
-        if (P.tails && P.dec_in_sample) {   // stochastic rows only (sd_verify)
-            if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true, true>), grid, dim3(kThreads), stream, P);
-            else SD_LAUNCH((k_sample<TDT, DDT, false, true, true, true>), grid, dim3(kThreads), stream, P);
-        } else if (P.tails) {
-            if (P.t_stoch) {
-                // poll-mode finish when the consumers (one per sequence) leave room for every producer
-                sd::Plan Q = P;
-                Q.spoll = sample_poll_ok(P.B, fast ? (const void*)k_sample<TDT, DDT, true, true, true>
-                                                   : (const void*)k_sample<TDT, DDT, false, true, true>);
-                if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, true, true>), grid, dim3(kThreads), stream, Q);
-                else SD_LAUNCH((k_sample<TDT, DDT, false, true, true>), grid, dim3(kThreads), stream, Q);
-            } else {
-                if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, false, true>), grid, dim3(kThreads), stream, P);
-                else SD_LAUNCH((k_sample<TDT, DDT, false, false, true>), grid, dim3(kThreads), stream, P);
-            }
-        } else {
-            const dim3 fin(P.B);
-            if (P.t_stoch) {
-                if (fast) {
-                    SD_LAUNCH((k_sample<TDT, DDT, true, true, false>), grid, dim3(kThreads), stream, P);
-                    SD_LAUNCH((k_sample_finish<TDT, DDT, true, true>), fin, dim3(kThreads), stream, P);
-                } else {
-                    SD_LAUNCH((k_sample<TDT, DDT, false, true, false>), grid, dim3(kThreads), stream, P);
-                    SD_LAUNCH((k_sample_finish<TDT, DDT, false, true>), fin, dim3(kThreads), stream, P);
-                }
-            } else {
-                if (fast) {
-                    SD_LAUNCH((k_sample<TDT, DDT, true, false, false>), grid, dim3(kThreads), stream, P);
-                    SD_LAUNCH((k_sample_finish<TDT, DDT, true, false>), fin, dim3(kThreads), stream, P);
-                } else {
-                    SD_LAUNCH((k_sample<TDT, DDT, false, false, false>), grid, dim3(kThreads), stream, P);
-                    SD_LAUNCH((k_sample_finish<TDT, DDT, false, false>), fin, dim3(kThreads), stream, P);
-                }
-            }
-        }
+        if (fast) SD_LAUNCH((k_sample<TDT, DDT, true, false>), grid, dim3(kThreads), stream, P);
+        else SD_LAUNCH((k_sample<TDT, DDT, false, false>), grid, dim3(kThreads), stream, P);
     }
     return SD_OK;
 }
@@ -3598,14 +3572,10 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
             per_cu = cus = 0;
         cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
     }
-    static const bool no_poll = getenv("SD_DRAW_NO_POLL") != nullptr;   // A/B switch: counter mode only
-    A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && !no_poll && poll_allowed();
+    A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && poll_allowed();
     A.spin_limit = P.spin_limit;
     A.status_or = P.status_or;
     A.ts = P.ts;
-    // XCD-affine placement (a row's spans and its poll exchange on one XCD group): SD_DRAW_AFFINE=1
-    static const int affine_env = getenv("SD_DRAW_AFFINE") ? atoi(getenv("SD_DRAW_AFFINE")) : 0;
-    A.affine = affine_env && P.B % 8 == 0;
     SD_LAUNCH((k_draw_lean<DT, NST, GREEDY>), dim3(A.n_span, P.B), dim3(kThreads), stream, A);
     return SD_OK;
 }
@@ -3614,23 +3584,21 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
 // caller runs k_stats + k_sample), < 0 a launch error.  Perf mode with the drafter stats from the
 // draws, no top-k / nucleus, 16-bit rows of one dtype, V <= 64 spans, every row 16-byte aligned, and
 // the whole grid resident (every workgroup polls).  Up to kLeanVerifyMaxB sequences by default;
-// SD_LEAN_VERIFY=0 turns it off, =1 allows any batch the occupancy check admits (A/B, tests).
+// SD_OPT_LEAN_VERIFY = 0 turns it off, = 1 allows any batch the occupancy check admits (A/B, tests).
 constexpr int kLeanVerifyMaxB = 8;
 
-static void lean_why(int k) {
-    const bool dbg = getenv("SD_LEAN_DEBUG") != nullptr;   // read per call: tests flip it
-    if (dbg) fprintf(stderr, k ? "launch_verify_lean: not applicable (%d)\n" : "launch_verify_lean: launched\n", k);
-}
+// why the lean verify was not taken (1..11), kept for diagnostics (a debugger / a printf build)
+thread_local int g_lean_why = 0;
+static void lean_why(int k) { g_lean_why = k; }
 
 int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
-    if (P0.noise.mode == SD_NOISE_STREAM || !P0.tails || P0.dec_in_sample) { lean_why(1); return 0; }
+    if (P0.noise.mode == SD_NOISE_STREAM) { lean_why(1); return 0; }
     // statistics: the target rows with the draws' drafter stats, or every row here; keep
     // predicates from this call's threshold search (P.keep) or the draws' (P.dkeep)
     if (P0.draft_is_probs || P0.stat_slots != (P0.dstats ? P0.n_tslots : P0.slots)) { lean_why(2); return 0; }
     if (P0.tdt != P0.ddt || (P0.tdt != SD_BF16 && P0.tdt != SD_F16)) { lean_why(3); return 0; }
     if (P0.n_tslots > sd::kLeanMaxT || P0.gamma > SD_LEAN_MAX_GAMMA || P0.B > kCntMax || !poll_allowed()) { lean_why(4); return 0; }
-    int mode = -1;
-    if (const char* e = getenv("SD_LEAN_VERIFY")) mode = atoi(e);
+    const int mode = opt(g_opt_lean);
     if (mode == 0 || (mode < 0 && P0.B > kLeanVerifyMaxB)) { lean_why(5); return 0; }
     constexpr int kSpan = kThreads * 8;
     const int n_span = (P0.V + kSpan - 1) / kSpan;
@@ -3690,12 +3658,10 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
 // sd_draw_stream.inc): 1 if launched, 0 if the shape needs the three-launch path (row statistics,
 // k_rowsample, k_sample_finalize), < 0 on a launch error.  Poll mode only: the grid's consumers
 // must leave room for every producer (the occupancy check), and sd_set_poll_policy must allow it;
-// SD_DRAW_STREAM=0 turns it off (A/B, tests).
+// SD_OPT_DRAW_STREAM = 0 turns it off (A/B, tests).
 int32_t launch_draw_stream(const sd::Plan& P, void* stream) {
     if (P.noise.mode != SD_NOISE_STREAM || !P.t_stoch || P.tT != 1.0f || P.t_keep || P.tdt == SD_F32) return 0;
-    if (P.token_prob || P.keep_out || P.B > kCntMax || !poll_allowed()) return 0;
-    if (const char* e = getenv("SD_DRAW_STREAM"))
-        if (!atoi(e)) return 0;
+    if (P.token_prob || P.keep_out || P.B > kCntMax || !poll_allowed() || opt(g_opt_draw_stream) == 0) return 0;
     const bool al = (reinterpret_cast<uintptr_t>(P.trow[0]) & 15) == 0 && (P.tstride * 2) % 16 == 0;
     const int n_span = (int)((P.V + kThreads * 8 - 1) / (kThreads * 8));
     if (!al || P.V < 8 || n_span > 128) return 0;
@@ -3739,11 +3705,10 @@ int32_t launch_draw_stream(const sd::Plan& P, void* stream) {
 // greedy sd_sample rows in one pass (k_draw_lean<GREEDY>): 1 if launched, 0 if the shape needs the
 // three-launch path (statistics, per-chunk argmax, finalize), < 0 on a launch error
 int32_t launch_greedy_lean(const sd::Plan& P, void* stream) {
-    static const bool off = getenv("SD_GREEDY_LEAN") && atoi(getenv("SD_GREEDY_LEAN")) == 0;   // A/B switch
     const bool fast = P.tT == 1.0f && !P.t_keep && P.tdt != SD_F32;
     const bool al = (reinterpret_cast<uintptr_t>(P.trow[0]) & 15) == 0 && (P.tstride * 2) % 16 == 0;
     const int64_t span = (int64_t)kThreads * 8;
-    if (off || !fast || !al || P.V < 8 || (P.V + span - 1) / span > 128) return 0;
+    if (!fast || !al || P.V < 8 || (P.V + span - 1) / span > 128) return 0;
     const int32_t st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 1, true>(P, stream)
                                         : launch_draw_lean_t<SD_F16, 1, true>(P, stream);
     return st == SD_OK ? 1 : st;
@@ -3753,14 +3718,12 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
     {
         const bool fast = P.tT == 1.0f && !P.t_keep && P.tdt != SD_F32;
         const bool al = (reinterpret_cast<uintptr_t>(P.trow[0]) & 15) == 0 && (P.tstride * 2) % 16 == 0;
-        // A/B switches, read once: SD_DRAW_LEAN_STAGES=2 (4096-element spans), SD_DRAW_NO_LEAN (k_draw only)
-        static const int nst_env = getenv("SD_DRAW_LEAN_STAGES") ? atoi(getenv("SD_DRAW_LEAN_STAGES")) : 1;
-        static const bool no_lean = getenv("SD_DRAW_NO_LEAN") != nullptr;
-        const int nst = nst_env == 2 ? 2 : 1;
-        const int64_t span = (int64_t)nst * kThreads * 8;
-        if (fast && al && P.V >= 8 && (P.V + span - 1) / span <= 128 && !no_lean) {
-            if (P.tdt == SD_BF16) return nst == 2 ? launch_draw_lean_t<SD_BF16, 2>(P, stream) : launch_draw_lean_t<SD_BF16, 1>(P, stream);
-            return nst == 2 ? launch_draw_lean_t<SD_F16, 2>(P, stream) : launch_draw_lean_t<SD_F16, 1>(P, stream);
+        // one 2048-element span per workgroup (4096-element spans measured slower)
+        const int64_t span = (int64_t)kThreads * 8;
+        if (fast && al && P.V >= 8 && (P.V + span - 1) / span <= 128) {
+            g_sample_path = SD_PATH_SAMPLE_DRAW_LEAN;
+            if (P.tdt == SD_BF16) return launch_draw_lean_t<SD_BF16, 1>(P, stream);
+            return launch_draw_lean_t<SD_F16, 1>(P, stream);
         }
     }
     // spans of NST stages (2048 elements each): 2 once the grid passes ~1024 workgroups
@@ -3768,14 +3731,13 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
     const int64_t stage = kThreads * 8;
     const int64_t nst_row = (P.V + stage - 1) / stage;
     int nst = P.B * nst_row <= 1024 ? 1 : 2;
-    if (const char* e = getenv("SD_DRAW_STAGES")) nst = atoi(e) == 4 ? 4 : (atoi(e) == 2 ? 2 : 1);
     if (P.tdt == SD_F32) nst = 2;   // fp32 stages hold 1024 elements: keep spans >= 2048 (workspace sizing)
     const int64_t step = kThreads * (int64_t)(P.tdt == SD_F32 ? 4 : 8);
     P.chunk = (int32_t)(nst * step);
     P.n_chunks = (int32_t)((P.V + P.chunk - 1) / P.chunk);
     P.rn_chunks = P.n_chunks;   // pick_chunk's count
     P.xcd_affine = P.B % 8 == 0;
-    if (getenv("SD_DRAW_NO_AFFINE")) P.xcd_affine = false;
+    g_sample_path = SD_PATH_SAMPLE_DRAW;
     if (P.tdt == SD_BF16) return launch_draw_dt<SD_BF16>(P, nst, stream);
     if (P.tdt == SD_F32) return launch_draw_dt<SD_F32>(P, nst, stream);
     return launch_draw_dt<SD_F16>(P, nst, stream);
@@ -3785,13 +3747,11 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
 // search + k_draw: PHILOX plain nucleus with top_p >= kNucMinP and T <= 1 (the proposal then keeps
 // >= top_p of its mass on the nucleus), 16-bit rows, no token_prob / row_stats / row_keep asked
 // (they need the nucleus' own normaliser), and the whole grid resident (its slices poll each other).
-// 1: launched; 0: not applicable.  SD_NUC_REJECT=0 turns it off (A/B, tests).
+// 1: launched; 0: not applicable.
 int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* stream) {
     if (P.noise.mode != SD_NOISE_PHILOX || proc.kind != SD_PROC_NUCLEUS) return 0;
     if (!(proc.top_p >= sd::kNucMinP) || !(proc.temperature <= 1.f) || P.tdt == SD_F32) return 0;
     if (P.token_prob || P.row_stats || P.keep_out || !poll_allowed()) return 0;
-    if (const char* e = getenv("SD_NUC_REJECT"))
-        if (!atoi(e)) return 0;
     // the verify's threshold search must cut this row with the same normaliser: its sub-slice mode
     const int nsl = (P.V + sd::kNucSlice - 1) / sd::kNucSlice;
     if (nsl > kWave || P.B > kCntMax || sd::kThrSlice != 4 * sd::kSubSlice) return 0;
@@ -3857,6 +3817,27 @@ int32_t sd_get_poll_policy(int32_t* allow_poll, int32_t* spin_limit_) {
 
 const char* sd_last_hip_error(void) { return hipGetErrorString(g_last_error); }
 
+int32_t sd_set_option(int32_t option, int32_t value) {
+    std::atomic<int>* o = option_slot(option);
+    if (!o) return SD_ERR_INVALID;
+    const bool ok = option == SD_OPT_FUSED_VERIFY ? (value >= 0 && value <= 2)
+                  : option == SD_OPT_LEAN_VERIFY ? (value >= -1 && value <= 1)
+                                                 : (value == 0 || value == 1);
+    if (!ok) return SD_ERR_INVALID;
+    o->store(value, std::memory_order_relaxed);
+    return SD_OK;
+}
+
+int32_t sd_get_option(int32_t option, int32_t* value) {
+    std::atomic<int>* o = option_slot(option);
+    if (!o || !value) return SD_ERR_INVALID;
+    *value = o->load(std::memory_order_relaxed);
+    return SD_OK;
+}
+
+int32_t sd_last_verify_path(void) { return g_verify_path; }
+int32_t sd_last_sample_path(void) { return g_sample_path; }
+
 const char* sd_status_string(int32_t s) {
     switch (s) {
         case SD_OK: return "ok";
@@ -3897,6 +3878,7 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
         (a->batch > kCntMax || (a->vocab + kThreads * kEptSmall - 1) / (kThreads * kEptSmall) > kTailChunks))
         return SD_ERR_UNSUPPORTED;
 
+    g_verify_path = SD_PATH_NONE;
     Plan P{};
     P.B = a->batch; P.gamma = a->gamma; P.V = a->vocab; P.rule = a->rule;
     P.n_tslots = n_t;
@@ -3953,29 +3935,21 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
 #ifdef SD_PHASE_TIMING
     if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
 #endif
-    // perf mode: decision / token in the last-arriving workgroups (tails) or in small own launches
-    P.tails = 1;
-    if (const char* e = getenv("SD_TAILS")) P.tails = atoi(e);
-    P.coh = perf && P.tails;
-    // stochastic rows, opt-in (SD_DEC_IN_SAMPLE=1): the decision moves from the k_stats tail into
-    // the sampler's workgroups.  Measured slower at the bench shape (step 63.9 vs 61.9 us: k_stats
-    // loses its 5 us tail but every k_sample workgroup pays ~7 us for the decision), so off.
-    P.dec_in_sample = 0;
-    if (const char* e = getenv("SD_DEC_IN_SAMPLE")) P.dec_in_sample = perf && P.tails && P.t_stoch && atoi(e);
+    // perf mode: decision / token in the last-arriving workgroups (tails)
+    P.coh = perf;
     P.xcd_affine = perf && P.B % 8 == 0;
-    if (const char* e = getenv("SD_XCD_AFFINE")) P.xcd_affine = P.xcd_affine && atoi(e);
     if (!a->prof_stats_begin) {   // the batch-1 / few-sequence verify in one launch (sd_verify_lean.inc)
         const int32_t st = launch_verify_lean(P, stream);
-        if (st) return st < 0 ? st : SD_OK;
+        if (st < 0) return st;
+        if (st) { g_verify_path = SD_PATH_VERIFY_LEAN; return SD_OK; }
     }
     // the verify in one launch (k_stats with a decider and samplers per sequence, fused_sampler): perf
-    // mode, stochastic target rows of one dtype, the drafter stats from the draws.  SD_FUSED=0 turns
-    // it off; by default it takes B >= 8 (fewer sequences: k_verify_lean above), SD_FUSED=2 any B.
-    if (perf && P.tails && !P.dec_in_sample && P.t_stoch && P.tdt == P.ddt && !P.draft_is_probs && P.dstats &&
+    // mode, stochastic target rows of one dtype, the drafter stats from the draws.  SD_OPT_FUSED_VERIFY
+    // = 0 turns it off; by default it takes B >= 8 (fewer sequences: k_verify_lean above), 2 any B.
+    if (perf && P.t_stoch && P.tdt == P.ddt && !P.draft_is_probs && P.dstats &&
         P.stat_slots == P.n_tslots && P.n_tslots <= kFastSlots && P.n_chunks <= kWave && P.B <= kCntMax &&
         !a->prof_stats_begin) {
-        int fmode = 1;
-        if (const char* e = getenv("SD_FUSED")) fmode = atoi(e);
+        const int fmode = opt(g_opt_fused);
         if (fmode == 2 || (fmode == 1 && P.B >= 8)) {
             Plan F = P;
             F.rchunk = kThreads * kFusedEpt;
@@ -3993,22 +3967,23 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
                 // before the pick's second pass, so the decider's Σ starts earlier (-0.45 us at B=32)
                 F.crec = F.drec + 2 * (size_t)P.B;
                 const int32_t st = launch_fused(F, stream);
-                if (st) return st < 0 ? st : SD_OK;
+                if (st < 0) return st;
+                if (st) { g_verify_path = SD_PATH_VERIFY_FUSED; return SD_OK; }
             }
         }
     }
     if (a->prof_stats_begin) (void)hipEventRecord((hipEvent_t)a->prof_stats_begin, (hipStream_t)stream);
     const int reps = a->prof_stats_begin && a->prof_stats_repeat > 1 ? a->prof_stats_repeat : 1;
     for (int rep = 0; rep < reps; ++rep)
-        if (int32_t st = launch_stats(P, stream, perf && P.tails && !P.dec_in_sample)) return st;
+        if (int32_t st = launch_stats(P, stream, perf)) return st;
     if (a->prof_stats_end) (void)hipEventRecord((hipEvent_t)a->prof_stats_end, (hipStream_t)stream);
-    if (perf && !P.tails) SD_LAUNCH(k_decide_perf, dim3(P.B), dim3(kThreads), stream, P);
     if (!perf) {   // parity mode: the reference's serial noise order
         SD_LAUNCH(k_decide, dim3(P.B), dim3(256), stream, P);
         SD_LAUNCH(k_walk, dim3(1), dim3(256), stream, P);
     }
     if (int32_t st = launch_resample(P, stream)) return st;   // perf mode: k_sample finalizes in its tail
     if (!perf) SD_LAUNCH(k_finalize, dim3(P.B), dim3(64), stream, P);
+    g_verify_path = perf ? SD_PATH_VERIFY_TWO_LAUNCH : SD_PATH_VERIFY_STREAM;
     return SD_OK;
 }
 
@@ -4046,7 +4021,12 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
 #ifdef SD_PHASE_TIMING
     if (const char* e = getenv("SD_TS_PTR")) P.ts = reinterpret_cast<uint64_t*>(strtoull(e, nullptr, 0));
 #endif
-    if (const int32_t st = launch_draw_nuc(P, a->proc, stream)) return st < 0 ? st : SD_OK;
+    g_sample_path = SD_PATH_NONE;
+    if (const int32_t st = launch_draw_nuc(P, a->proc, stream)) {
+        if (st < 0) return st;
+        g_sample_path = SD_PATH_SAMPLE_NUCLEUS;
+        return SD_OK;
+    }
     if (P.t_keep) {
         const int32_t st = launch_threshold(P, a->proc, a->proc, stream);
         if (st != SD_OK) return st;
@@ -4055,16 +4035,21 @@ int32_t sd_sample(const sd_sample_args* a, void* stream) {
         if (P.B > kCntMax || max_chunks(P.V) > kTailChunks) return SD_ERR_UNSUPPORTED;
         return launch_draw(P, stream);   // one pass; the row's last arrival writes the outputs
     }
-    if (const int32_t st = launch_draw_stream(P, stream)) return st < 0 ? st : SD_OK;   // STREAM, one pass
+    if (const int32_t st = launch_draw_stream(P, stream)) {   // STREAM, one pass
+        if (st < 0) return st;
+        g_sample_path = SD_PATH_SAMPLE_STREAM;
+        return SD_OK;
+    }
     if (!P.t_stoch && P.B <= kCntMax) {   // greedy (either noise mode: no noise is drawn)
         const int32_t st = launch_greedy_lean(P, stream);
         if (st < 0) return st;
-        if (st == 1) return SD_OK;
+        if (st == 1) { g_sample_path = SD_PATH_SAMPLE_GREEDY_LEAN; return SD_OK; }
     }
     set_rchunks(P);
     if (int32_t st = launch_stats(P, stream)) return st;
     if (int32_t st = launch_rowsample(P, stream)) return st;
     SD_LAUNCH(k_sample_finalize, dim3(P.B), dim3(64), stream, P);
+    g_sample_path = SD_PATH_SAMPLE_MULTI;
     return SD_OK;
 }
 

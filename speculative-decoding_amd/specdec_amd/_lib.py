@@ -9,8 +9,9 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 9
-SD_MAX_GAMMA = 32
+SD_ABI_VERSION = 10
+SD_MAX_GAMMA = 32           # drafts per call (ops.verify / ngram_verify chunk longer windows)
+SD_NGRAM_MAX_FILLER = 64
 
 SD_OK, SD_ERR_INVALID, SD_ERR_WORKSPACE, SD_ERR_LAUNCH, SD_ERR_UNSUPPORTED = 0, -1, -2, -3, -4
 SD_F32, SD_BF16, SD_F16 = 0, 1, 2
@@ -31,6 +32,18 @@ SD_ROW_EXCHANGE_TIMEOUT = 0x200
 # the bits that make a row's outputs unusable (the reference raises there): status_or collects them
 SD_ROW_ERROR_MASK = SD_ROW_INVALID_DIST | SD_ROW_NOISE_OVERRUN | SD_ROW_EXCHANGE_TIMEOUT
 
+# dispatch options (sd_set_option) and the paths sd_last_*_path reports
+SD_OPT_FUSED_VERIFY, SD_OPT_LEAN_VERIFY, SD_OPT_THRESHOLD_POLL, SD_OPT_DRAW_STREAM = 1, 2, 3, 4
+SD_PATH_NONE = 0
+SD_PATH_VERIFY_LEAN, SD_PATH_VERIFY_FUSED, SD_PATH_VERIFY_TWO_LAUNCH, SD_PATH_VERIFY_STREAM = 1, 2, 3, 4
+SD_PATH_SAMPLE_DRAW_LEAN, SD_PATH_SAMPLE_DRAW, SD_PATH_SAMPLE_NUCLEUS, SD_PATH_SAMPLE_STREAM = 16, 17, 18, 19
+SD_PATH_SAMPLE_GREEDY_LEAN, SD_PATH_SAMPLE_MULTI = 20, 21
+PATH_NAMES = {SD_PATH_NONE: "none", SD_PATH_VERIFY_LEAN: "k_verify_lean", SD_PATH_VERIFY_FUSED: "k_verify_fused",
+              SD_PATH_VERIFY_TWO_LAUNCH: "k_stats+k_sample", SD_PATH_VERIFY_STREAM: "stream",
+              SD_PATH_SAMPLE_DRAW_LEAN: "k_draw_lean", SD_PATH_SAMPLE_DRAW: "k_draw", SD_PATH_SAMPLE_NUCLEUS: "k_draw_nuc",
+              SD_PATH_SAMPLE_STREAM: "k_draw_stream", SD_PATH_SAMPLE_GREEDY_LEAN: "k_draw_lean<greedy>",
+              SD_PATH_SAMPLE_MULTI: "k_stats+k_rowsample+k_sample_finalize"}
+
 # SPECDEC_LIB selects another in-tree build of the same ABI (e.g. the phase-timing variant)
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), os.environ.get("SPECDEC_LIB", "libspecdec.so"))
 
@@ -41,7 +54,8 @@ EXPORTS = ("sd_abi_version", "sd_status_string", "sd_last_hip_error", "sd_verify
            "sd_ngram_store_has_gram", "sd_ngram_store_draft",
            "sd_mt19937_state_from_torch", "sd_mt19937_state_to_torch", "sd_mt19937_jump_table",
            "sd_mt19937_char_poly", "sd_mt19937_fill_substreams", "sd_mt19937_generate_workspace_size",
-           "sd_mt19937_generate", "sd_mt19937_commit", "sd_set_poll_policy", "sd_get_poll_policy")
+           "sd_mt19937_generate", "sd_mt19937_commit", "sd_set_poll_policy", "sd_get_poll_policy",
+           "sd_set_option", "sd_get_option", "sd_last_verify_path", "sd_last_sample_path")
 
 SD_MT_JUMP_WORDS = 320
 SD_MT_JUMP_CHUNKS = 16
@@ -204,6 +218,13 @@ def _load():
     lib.sd_set_poll_policy.argtypes = [C.c_int32, C.c_int32]
     lib.sd_get_poll_policy.restype = C.c_int32
     lib.sd_get_poll_policy.argtypes = [C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    lib.sd_set_option.restype = C.c_int32
+    lib.sd_set_option.argtypes = [C.c_int32, C.c_int32]
+    lib.sd_get_option.restype = C.c_int32
+    lib.sd_get_option.argtypes = [C.c_int32, C.POINTER(C.c_int32)]
+    for name in ("sd_last_verify_path", "sd_last_sample_path"):
+        getattr(lib, name).restype = C.c_int32
+        getattr(lib, name).argtypes = []
     P = C.POINTER(sd_ngram_store)
     for name, args in (("sd_ngram_store_initialize", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_int64, C.c_void_p]),
                        ("sd_ngram_store_update", [P, C.c_void_p, C.c_int32, C.c_int32, C.c_int64, C.c_void_p, C.c_int32,
@@ -247,6 +268,43 @@ def get_poll_policy():
     a, s = C.c_int32(), C.c_int32()
     check(lib.sd_get_poll_policy(C.byref(a), C.byref(s)), "sd_get_poll_policy")
     return bool(a.value), int(s.value)
+
+
+def set_option(option: int, value: int) -> None:
+    """sd_set_option: a process-wide dispatch switch (SD_OPT_*) between equivalent kernel paths."""
+    check(lib.sd_set_option(int(option), int(value)), "sd_set_option")
+
+
+def get_option(option: int) -> int:
+    v = C.c_int32()
+    check(lib.sd_get_option(int(option), C.byref(v)), "sd_get_option")
+    return int(v.value)
+
+
+class option:
+    """Context manager: ``with option(SD_OPT_FUSED_VERIFY, 0): ...`` restores the old value after."""
+
+    def __init__(self, opt: int, value: int):
+        self.opt, self.value = opt, value
+
+    def __enter__(self):
+        self.old = get_option(self.opt)
+        set_option(self.opt, self.value)
+        return self
+
+    def __exit__(self, *exc):
+        set_option(self.opt, self.old)
+        return False
+
+
+def last_verify_path() -> int:
+    """SD_PATH_* of this thread's last successful sd_verify (which kernels ran)."""
+    return int(lib.sd_last_verify_path())
+
+
+def last_sample_path() -> int:
+    """SD_PATH_* of this thread's last successful sd_sample."""
+    return int(lib.sd_last_sample_path())
 
 
 class RowError(RuntimeError):

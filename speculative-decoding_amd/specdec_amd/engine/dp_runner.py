@@ -284,7 +284,9 @@ def infer_batches_dp(ctx, prompt_batches: Sequence[List[str]], dist=None, seed: 
     ``reseed(seed); infer_batch(ctx, prompts)`` for batches r, r + world, ...; every rank returns
     the ``(spec_metrics, target_metrics)`` pair of EVERY batch, in batch order (what the reference
     appends to its BenchmarkResults).  A failed batch is ``(None, None)``, as infer_batch returns it
-    (:144-146)."""
+    (:144-146).  An exception that escapes infer_batch on one rank (tokenization, the chat template,
+    a device copy, the target-only path) is held until after the gather and then raised on EVERY
+    rank, as generate_batches_dp does — no rank is left waiting in the gather."""
     from .infer_engine import infer_batch
     world, rank = _world(dist)
     dev = getattr(ctx, "drafter_device", None) or getattr(ctx, "target_device", None)
@@ -292,6 +294,9 @@ def infer_batches_dp(ctx, prompt_batches: Sequence[List[str]], dist=None, seed: 
         configure_residency(dist, dev)
     mine = []
     for i in batches_of_rank(len(prompt_batches), world, rank):
-        reseed(seed)
-        mine.append((i, True, infer_batch(ctx, list(prompt_batches[i]))))
+        try:
+            reseed(seed)
+            mine.append((i, True, infer_batch(ctx, list(prompt_batches[i]))))
+        except Exception as e:   # reported after the gather
+            mine.append((i, False, f"rank {rank} batch {i}: {type(e).__name__}: {e}"))
     return _gather_in_order(mine, len(prompt_batches), dist, "infer_batches_dp")

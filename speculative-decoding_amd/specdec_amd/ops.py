@@ -49,14 +49,29 @@ class ProcSpec:
 PLAIN_SOFTMAX = ProcSpec("multinomial", 1.0)   # engine/infer_engine.py:241,276 (T=1, no processor)
 
 
+# the processor protocol's behaviour (utils/logits_processor.py:7-23): a subclass that redefines one
+# of these computes something the kernels do not, so it is refused, never run as its base class
+_PROC_BEHAVIOUR = ("__call__", "_process", "sample")
+
+
 def proc_spec(proc) -> ProcSpec:
-    """ProcSpec of one of the five processors (ours, the reference's, or a ProcSpec)."""
+    """ProcSpec of one of the five processors (ours, the reference's, or a ProcSpec).
+
+    A subclass of a known processor is accepted only if it changes no behaviour (e.g. a constructor
+    that fixes parameters); one that overrides ``__call__``, ``_process`` or ``sample`` raises
+    TypeError — the kernels fuse the five processors' arithmetic and cannot run user code."""
     if isinstance(proc, ProcSpec):
         return proc
     name = type(proc).__name__
-    for cls in type(proc).__mro__:
+    mro = type(proc).__mro__
+    for i, cls in enumerate(mro):
         if cls.__name__ in _CLASS_KIND:
             name = cls.__name__
+            for sub in mro[:i]:
+                over = [m for m in _PROC_BEHAVIOUR if m in vars(sub)]
+                if over:
+                    raise TypeError(f"unsupported logits processor {type(proc).__name__}: {sub.__name__} overrides "
+                                    f"{', '.join(over)} of {name}, which the fused kernels cannot run")
             break
     if name not in _CLASS_KIND:
         raise TypeError(f"unsupported logits processor {type(proc).__name__}")
@@ -245,8 +260,15 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
     tokens emitted) to every row's pair (the A12 bookkeeping, kept on the device).
     """
     gamma = len(draft_rows)
-    if not 1 <= gamma <= _lib.SD_MAX_GAMMA:
-        raise ValueError(f"gamma must be in [1, {_lib.SD_MAX_GAMMA}], got {gamma}")
+    if gamma > _lib.SD_MAX_GAMMA:   # the reference takes any γ: windows of <= SD_MAX_GAMMA drafts (chunked.py)
+        if prof_events is not None:
+            raise ValueError("prof_events needs gamma <= SD_MAX_GAMMA")
+        from .chunked import verify_chunked
+        return verify_chunked(target_rows, draft_rows, draft_tokens, rule, target_proc, draft_proc, noise,
+                              stop_tokens, skip_sample_adjustment, draft_is_probs, active, engine_state, sync_noise,
+                              row_base, draft_row_stats, draft_row_keep, status_or, row_counts)
+    if not 1 <= gamma:
+        raise ValueError(f"gamma must be >= 1, got {gamma}")
     n_t = gamma + 1 if rule == _lib.SD_RULE_SPEC else gamma
     if len(target_rows) != n_t:
         raise ValueError(f"expected {n_t} target rows, got {len(target_rows)}")
@@ -373,10 +395,14 @@ def ngram_verify(target_rows: Sequence[torch.Tensor], draft_tokens: Optional[tor
     advances by the words the draws consumed (the reference's order), one device->host read."""
     spec = proc_spec(proc)
     gamma = len(target_rows) - 1
-    if not 0 <= gamma <= _lib.SD_MAX_GAMMA:
-        raise ValueError(f"gamma must be in [0, {_lib.SD_MAX_GAMMA}], got {gamma}")
-    if not 0 <= filler_k <= 8:
-        raise ValueError("filler_k must be in [0, 8]")
+    if not 0 <= filler_k <= _lib.SD_NGRAM_MAX_FILLER:
+        raise ValueError(f"filler_k must be in [0, {_lib.SD_NGRAM_MAX_FILLER}]")
+    if gamma > _lib.SD_MAX_GAMMA:   # the reference takes any γ: windows of <= SD_MAX_GAMMA drafts (chunked.py)
+        from .chunked import ngram_verify_chunked
+        return ngram_verify_chunked(target_rows, draft_tokens, proc, noise, stop_tokens, filler_k, sync_noise,
+                                    row_base, status_or)
+    if not 0 <= gamma:
+        raise ValueError(f"gamma must be >= 0, got {gamma}")
     B, V = target_rows[0].shape
     dev = target_rows[0].device
     tdt = target_rows[0].dtype

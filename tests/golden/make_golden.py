@@ -67,13 +67,20 @@ SPEC_CASES = [
     # drafter = target + N(0, 0.05^2): drafts are accepted deep into the γ = 24 window
     ("multi_t1_g24_bf16_close", 4096, "bf16", 24, ("multinomial", 1.0, 0, 1.0), 96, [1], False, [0, 1], 0.05),
     ("greedy_g32_bf16_close", 4096, "bf16", 32, ("greedy", 1.0, 0, 1.0), 96, [1], False, [0], 0.05),
+    # γ beyond SD_MAX_GAMMA = 32: specdec_amd.ops verifies the window in chunks of <= 32 drafts
+    ("multi_t1_g48_bf16_close", 4096, "bf16", 48, ("multinomial", 1.0, 0, 1.0), 160, [1], False, [0, 1, 2], 0.05),
+    ("greedy_g40_bf16_close", 4096, "bf16", 40, ("greedy", 1.0, 0, 1.0), 120, [1], False, [0], 0.05),
+    ("nucleus09_g40_bf16_close", 4096, "bf16", 40, ("nucleus", 1.0, 0, 0.9), 120, [1], False, [0], 0.05),
+    ("multi_t1_g48_bf16_close_eos", 4096, "bf16", 48, ("multinomial", 1.0, 0, 1.0), 200, "likely", False,
+     [0, 1], 0.05),
+    ("multi_t1_g40_bf16", 4096, "bf16", 40, ("multinomial", 1.0, 0, 1.0), 100, [1], False, [0]),
 ]
 
 # The engine re-feeds the last prompt token to the drafter after its prefill (engine/infer_engine.py:206,231),
 # so drafter and target see it at different positions; pos_mult=0 banks (logits depend on the token only)
 # keep their distributions aligned so the accept branch is exercised.
 ENGINE_CASES = [
-    # name, V, dtype, B, gamma, gen_len, end_tokens, seeds[, pos_mult]
+    # name, V, dtype, B, gamma, gen_len, end_tokens, seeds[, pos_mult[, sigma]]
     ("b1_g4_bf16_pos7", 4096, "bf16", 1, 4, 32, [1], [0], 7),
     ("b1_g4_bf16", 4096, "bf16", 1, 4, 32, [1], [0, 1]),
     ("b1_g4_fp32", 4096, "fp32", 1, 4, 32, [1], [0]),
@@ -86,6 +93,11 @@ ENGINE_CASES = [
     ("llama_b2_g4_fp32", 128256, "fp32", 2, 4, 12, [128001, 128009], [0]),
     ("b4_g20_fp32", 2048, "fp32", 4, 20, 48, [1], [0]),
     ("b3_g32_fp32_eos", 2048, "fp32", 3, 32, 70, "likely", [1]),
+    # γ beyond SD_MAX_GAMMA = 32 (chunked windows); drafter = target + N(0, 0.05^2): accepts reach chunk 2
+    ("b3_g48_fp32_close", 2048, "fp32", 3, 48, 120, [1], [0, 1], 0, 0.05),
+    ("b1_g48_bf16_close", 4096, "bf16", 1, 48, 120, [1], [0], 0, 0.05),
+    ("b4_g40_fp32_close_eos", 2048, "fp32", 4, 40, 120, "likely", [1, 2], 0, 0.05),
+    ("b2_g40_fp32", 2048, "fp32", 2, 40, 80, [1], [0]),
 ]
 
 # ngram-assisted loop (rule A11): FakeLM target, the reference's n-gram storages as the drafter
@@ -104,6 +116,12 @@ NGRAM_CASES = [
     ("ng_llama_nucleus_g8", 128256, "bf16", ("multi", 3), 8, ("nucleus", 1.0, 0, 0.9), 3, False, 24,
      [128001, 128009], [0, 1, 2]),
     ("ng_multi_g20_n3", 4096, "bf16", ("multi", 3), 20, ("multinomial", 1.0, 0, 1.0), 3, False, 60, [1], [0]),
+    # filler top-k beyond 8 (SD_NGRAM_MAX_FILLER = 64) and γ' beyond SD_MAX_GAMMA (chunked windows)
+    ("ng_multi_g4_n3_f16", 4096, "bf16", ("multi", 3), 4, ("multinomial", 1.0, 0, 1.0), 16, False, 40, [1], [0, 1]),
+    ("ng_greedy_g8_n3_f40", 4096, "bf16", ("multi", 3), 8, ("greedy", 1.0, 0, 1.0), 40, False, 40, [1], [0]),
+    ("ng_greedy_g40_n3", 4096, "bf16", ("multi", 3), 40, ("greedy", 1.0, 0, 1.0), 3, False, 160, [1], [0, 1]),
+    ("ng_multi_g48_n3_f16", 4096, "bf16", ("multi", 3), 48, ("multinomial", 1.0, 0, 1.0), 16, False, 160, [1],
+     [0, 1]),
 ]
 
 DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
@@ -185,7 +203,8 @@ def main(only=None):
         if not keep(name):
             continue
         pos_mult = pm[0] if pm else 0
-        target, drafter = make_pair(V, dtype=DT[dt], pos_mult=pos_mult)
+        sigma = pm[1] if len(pm) > 1 else 1.0
+        target, drafter = make_pair(V, dtype=DT[dt], pos_mult=pos_mult, sigma=sigma)
         if ends == "likely":
             ends = likely_tokens(target)
         for seed in seeds:
@@ -195,7 +214,7 @@ def main(only=None):
                                   end_tokens=ends, target_device="cpu")
             torch.manual_seed(seed)
             rec = dict(vocab=V, dtype=dt, batch=B, gamma=gamma, gen_len=gen_len, end_tokens=ends, seed=seed,
-                       pos_mult=pos_mult,
+                       pos_mult=pos_mult, sigma=sigma,
                        prompt=ids.tolist(), target_digest=bank_digest(target),
                        drafter_digest=bank_digest(drafter))
             try:

@@ -197,6 +197,20 @@ def _batch_worker(rank, world, port, n_batches, seed, out):
             rec["fail"] = "no error"
         except RuntimeError as e:
             rec["fail"] = str(e)
+
+        # infer_batch raising outside the decode (tokenization, chat template, .to(device)) on one
+        # rank's batch: every rank raises after the gather, none is left waiting in it
+        def raising_infer(ctx, prompts):
+            if len(prompts) == 2:                # batch 1, on rank 1
+                raise ValueError("chat template missing")
+            return (len(prompts), 0.0), None
+        infer_engine.infer_batch = raising_infer
+        try:
+            dp_runner.infer_batches_dp(SimpleNamespace(), [["p"] * (k + 1) for k in range(n_batches)], dist,
+                                       seed=seed)
+            rec["infer_fail"] = "no error"
+        except RuntimeError as e:
+            rec["infer_fail"] = str(e)
         out.put((rank, rec))
     finally:
         dist.destroy_process_group()
@@ -231,6 +245,7 @@ def test_batch_level_dp_is_bit_exact_under_stream_noise():
             assert rec["batches"] == want, (n_batches, rank)
             assert [tuple(p[0]) for p in rec["pairs"]] == [p[0] for p in want_pairs]
             assert "batch 1" in rec["fail"] and "rank 1" in rec["fail"]
+            assert "rank 1 batch 1: ValueError: chat template missing" in rec["infer_fail"], rec["infer_fail"]
 
 
 def test_dp_runner_forwards_the_graph_paths_first_token_time(monkeypatch):

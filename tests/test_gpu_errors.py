@@ -187,8 +187,8 @@ def test_thresholds_exact_when_every_slice_poll_gives_up(monkeypatch):
     """k_thr_hist in poll mode with every slice-max poll giving up: every slice skips its histogram
     flush and the row takes the radix descent — the keep sets still equal the exact oracle (a
     row is never cut from a partial histogram)."""
-    from specdec_amd import ops
-    monkeypatch.setenv("SD_THR_POLL", "1")
+    from specdec_amd import _lib, ops
+    assert _lib.get_option(_lib.SD_OPT_THRESHOLD_POLL) == 1
     g = torch.Generator().manual_seed(4)
     rows = (torch.randn(3, 128256, generator=g) * 3).to(torch.bfloat16)
     for proc in (ref.Processor("nucleus", 1.0, 0, 0.9), ref.Processor("topk", 1.0, 50)):

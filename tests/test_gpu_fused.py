@@ -1,12 +1,14 @@
 """The one-launch fused verify (k_verify_fused: spans, a decider and two-chunk samplers per sequence,
-csrc/specdec_kernels.hip) against the two-launch verify (k_stats + k_sample, SD_FUSED=0) on identical
+csrc/specdec_kernels.hip) against the two-launch verify (k_stats + k_sample, SD_OPT_FUSED_VERIFY = 0) on identical
 inputs and Philox noise.
 
 Both take the decision from the same row statistics (the same k_stats span code and decide tail),
 sample the decided row in the same 2048-element chunks with the same chunk uniforms and pick the
 chunk with the same fp64 scan, so their outputs are identical, row for row — including the engine
-state the verify updates in place and the per-row counters.  Also: the path is taken (B >= 8) and
-a poll that gives up (spin limit < 0) flags rows instead of returning tokens."""
+state the verify updates in place and the per-row counters.  Also: the path is taken (B >= 8,
+sd_last_verify_path) and a poll that gives up (spin limit < 0) flags rows instead of returning tokens.
+The fused kernel's outputs are also checked against the oracle directly: tests/test_gpu_perfmode.py
+(the accept walks with the drafter stats from the draws, and the residual / bonus chi-squares)."""
 import contextlib
 
 import pytest
@@ -16,19 +18,9 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@contextlib.contextmanager
-def env(**kv):
-    import os
-    old = {k: os.environ.get(k) for k in kv}
-    os.environ.update({k: str(v) for k, v in kv.items()})
-    try:
-        yield
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+def fused(value):
+    from specdec_amd import _lib
+    return _lib.option(_lib.SD_OPT_FUSED_VERIFY, value)
 
 
 def inputs(B, g, V, rule, seed):
@@ -65,6 +57,7 @@ def run(tl, dl, rule, spec, seed, engine=False, verify_ctx=contextlib.nullcontex
                          draft_row_keep=keep, row_counts=counts, **extra)
         torch.cuda.synchronize()
     res = {k: getattr(out, k).cpu() for k in ("n_accepted", "next_token", "row_status", "resample_mass")}
+    res["path"] = torch.tensor(_lib.last_verify_path())
     res["counts"] = counts.cpu()
     if state is not None:
         res.update({k: v.cpu() for k, v in state.items() if torch.is_tensor(v)})
@@ -83,10 +76,13 @@ def test_fused_verify_equals_two_launch_verify(B, V, rule, proc):
     seed = 31 * B + V % 89 + (1 if rule == "spec" else 2)
     tl, dl = inputs(B, 4, V, rule, seed)
     engine = rule == "engine"
-    with env(SD_FUSED=1):
+    from specdec_amd import _lib
+    with fused(1):
         a = run(tl, dl, rule, spec, seed, engine)
-    with env(SD_FUSED=0):
+    with fused(0):
         b = run(tl, dl, rule, spec, seed, engine)
+    assert int(a.pop("path")) == _lib.SD_PATH_VERIFY_FUSED
+    assert int(b.pop("path")) == _lib.SD_PATH_VERIFY_TWO_LAUNCH
     for k in a:
         assert torch.equal(a[k].nan_to_num(), b[k].nan_to_num()), (k, a[k], b[k])
     active = (torch.arange(B) % 5 != 3) if engine else torch.ones(B, dtype=torch.bool)
@@ -112,7 +108,8 @@ def test_fused_verify_polls_are_bounded():
         finally:
             set_poll_policy(*old)
 
-    with env(SD_FUSED=1):
+    with fused(1):
         a = run(tl, dl, "engine", spec, 5, verify_ctx=no_polls)
+    assert int(a["path"]) == _lib.SD_PATH_VERIFY_FUSED
     assert (a["row_status"] & _lib.SD_ROW_EXCHANGE_TIMEOUT).all()
     assert (a["row_status"] & _lib.SD_ROW_INVALID_DIST).all()

@@ -44,8 +44,8 @@ KINDS = {
 def sd():
     import specdec_amd
     from specdec_amd import _lib, ops
-    from specdec_amd.noise import StreamNoise
-    return SimpleNamespace(lib=_lib, ops=ops, StreamNoise=StreamNoise, pkg=specdec_amd)
+    from specdec_amd.noise import PhiloxNoise, StreamNoise
+    return SimpleNamespace(lib=_lib, ops=ops, StreamNoise=StreamNoise, PhiloxNoise=PhiloxNoise, pkg=specdec_amd)
 
 
 def spec_of(sd, p: ref.Processor):
@@ -117,7 +117,8 @@ def run_spec_oracle(tl, dl, ids, proc, gen, stops, skip=False, exact=False):
         q = ref.process(dl[b], proc, exact).float()
         r = torch.rand(g, generator=gen)
         n, p = ref.spec_accept(tl[b], q, ids[b].tolist(), proc, r, exact)
-        hit = [j for j in range(n) if int(ids[b, j]) in stops]
+        hit = [ref.stop_location(ids[b, :n].tolist(), stops)]
+        hit = [h for h in hit if h >= 0]
         if hit:
             res.append(dict(n=n, x=-1, stop=hit[0], mass=float("nan")))
             continue
@@ -237,6 +238,57 @@ def test_spec_verify_skip_sample_adjustment(sd):
         check_spec(sd, tl, dl, ids, proc, 50 + seed, skip=True)
 
 
+@pytest.mark.parametrize("B,gamma,kind,seed", [(1, 40, "multi_t1", 70), (1, 48, "greedy", 71), (3, 40, "multi_t1", 72),
+                                              (2, 64, "multi_t07", 73), (1, 33, "nucleus09", 74)])
+def test_spec_verify_chunked_window(sd, B, gamma, kind, seed):
+    """γ > SD_MAX_GAMMA (specdec_amd/chunked.py): the window in chunks of <= 32 drafts equals one
+    reference verify over all γ — accept count, token, prune lengths and the generator's advance
+    (γ uniforms, then the sample's 2V words).  Drafter = target + N(0, 0.05²), so the accept walks
+    cross the chunk boundary; one row's last draft off-distribution so rejects land late."""
+    proc = KINDS[kind]
+    tl, dl, ids = draft_case(B, gamma, 4096, torch.bfloat16, seed, proc, sigma=0.05)
+    st = check_spec(sd, tl, dl, ids, proc, seed)
+    assert all(s & sd.lib.SD_ROW_DONE for s in st)
+
+
+def test_spec_verify_chunked_window_stops(sd):
+    """A stop token in the second chunk's accepted drafts, with the walk still accepting: the stop
+    return, at the reference's position (the first-listed stop token that occurs)."""
+    proc = KINDS["greedy"]
+    tl = rand_logits((1, 41, 4096), torch.bfloat16, 75)
+    dl = tl[:, :40].clone()
+    ids = torch.stack([ref.process(dl[0], proc).argmax(-1)])
+    st = check_spec(sd, tl, dl, ids, proc, 75, stops=[int(ids[0, 35]), int(ids[0, 37])])
+    assert st[0] & sd.lib.SD_ROW_STOP_IN_DRAFTS
+
+
+@pytest.mark.parametrize("fused", [0, 1], ids=["two-launch", "fused"])
+def test_spec_verify_stop_list_order(sd, fused):
+    """sampling/speculative_decoding.py:150-152 scans eq(drafts[1, n], stop_tokens[S, 1]) row-major:
+    with several listed stop tokens among the accepted drafts the return is at the first-LISTED one
+    (here the later position), not the earliest stop position.  STREAM (check_spec) and Philox, the
+    latter with the drafter stats from draws so B = 8 takes the one-launch kernels."""
+    proc = KINDS["greedy"]
+    tl = rand_logits((8, 9, 4096), torch.bfloat16, 76)
+    dl = tl[:, :8].clone()
+    ids = torch.stack([ref.process(dl[b], proc).argmax(-1) for b in range(8)])
+    stops = [int(ids[0, 5]), int(ids[0, 2])]
+    st = check_spec(sd, tl, dl, ids, proc, 76, stops=stops)
+    assert st[0] & sd.lib.SD_ROW_STOP_IN_DRAFTS
+    tld, dld, idd = tl.to(DEV), dl.to(DEV), ids.to(DEV)
+    stats = torch.empty(8, 8, 2, device=DEV)
+    for d in range(8):
+        sd.ops.sample_rows(dld[:, d], spec_of(sd, proc), sd.PhiloxNoise(seed=1), row_stats_out=stats[d])
+    with sd.lib.option(sd.lib.SD_OPT_FUSED_VERIFY, 2 if fused else 0), sd.lib.option(sd.lib.SD_OPT_LEAN_VERIFY, 0):
+        out = sd.ops.verify([tld[:, t] for t in range(9)], [dld[:, d] for d in range(8)], idd, sd.lib.SD_RULE_SPEC,
+                            spec_of(sd, proc), spec_of(sd, proc), sd.PhiloxNoise(seed=5),
+                            torch.tensor(stops, dtype=torch.long, device=DEV), draft_row_stats=stats)
+    for b in range(8):
+        want = ref.stop_location(ids[b].tolist(), stops)
+        assert int(out.stop_index[b]) == want, (b, int(out.stop_index[b]), want)
+    assert int(out.stop_index[0]) == 5
+
+
 @pytest.mark.parametrize("seed", range(12))
 def test_spec_verify_many_seeds(sd, seed):
     proc = [KINDS["greedy"], KINDS["multi_t1"], KINDS["multi_t07"]][seed % 3]
@@ -257,11 +309,25 @@ ENGINE_GRID = [
 
 @pytest.mark.parametrize("B,gamma,V,dtype,seed", ENGINE_GRID)
 def test_engine_verify_matches_oracle(sd, B, gamma, V, dtype, seed):
+    _engine_case(sd, B, gamma, V, dtype, seed)
+
+
+@pytest.mark.parametrize("B,gamma,V,dtype,seed", [(3, 40, 2048, torch.float32, 6), (4, 48, 4096, torch.bfloat16, 7),
+                                                  (1, 70, 2048, torch.float32, 8)])
+def test_engine_verify_chunked_window(sd, B, gamma, V, dtype, seed):
+    """γ > SD_MAX_GAMMA (specdec_amd/chunked.py): the engine window in chunks of <= 32 drafts, row by
+    row under STREAM, equals the reference's walk over all γ (engine state, counts, generator)."""
+    _engine_case(sd, B, gamma, V, dtype, seed, sigma=0.05, late_stop=True)
+
+
+def _engine_case(sd, B, gamma, V, dtype, seed, sigma=1.0, late_stop=False):
     plain = ref.Processor("multinomial", 1.0)
-    tl, dl, ids = draft_case(B, gamma, V, dtype, seed, plain)
+    tl, dl, ids = draft_case(B, gamma, V, dtype, seed, plain, sigma=sigma)
     tl = tl[:, :gamma]
     gen_len, step = gamma * 3, gamma
     end_tokens = [int(ids[0, min(1, gamma - 1)]), int(ids[min(2, B - 1), 0])]
+    if late_stop:   # an end token past the first chunk (row 0), so the walks cross the chunk boundary
+        end_tokens = [int(ids[0, gamma - 4])]
     finished = torch.zeros(B, dtype=torch.bool)
     finished[B // 2] = True if B > 2 else False
     generated = torch.zeros(B, gen_len, dtype=torch.long)
@@ -424,7 +490,8 @@ def test_speculative_generate_matches_reference(sd, case):
 def test_batch_speculative_generate_matches_reference(sd, case):
     from specdec_amd.engine.infer_engine import batch_speculative_generate
     c = ENGINE[case]
-    target, drafter = make_pair(c["vocab"], dtype=DT[c["dtype"]], device=DEV, pos_mult=c["pos_mult"])
+    target, drafter = make_pair(c["vocab"], dtype=DT[c["dtype"]], device=DEV, pos_mult=c["pos_mult"],
+                                sigma=c.get("sigma", 1.0))
     ids = torch.tensor(c["prompt"], dtype=torch.long, device=DEV)
     ctx = SimpleNamespace(drafter=drafter, target=target, gamma=c["gamma"], gen_len=c["gen_len"],
                           end_tokens=c["end_tokens"])
@@ -432,7 +499,7 @@ def test_batch_speculative_generate_matches_reference(sd, case):
     outs, rates = batch_speculative_generate(ctx, ids, torch.ones_like(ids), c["batch"])
     if c["raised"]:
         # the reference crashed here (bf16, B>=2); the drop-in must run and agree with the oracle
-        tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]], pos_mult=c["pos_mult"])
+        tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]], pos_mult=c["pos_mult"], sigma=c.get("sigma", 1.0))
         octx = SimpleNamespace(drafter=dc, target=tc, gamma=c["gamma"], gen_len=c["gen_len"],
                                end_tokens=c["end_tokens"])
         torch.manual_seed(c["seed"])
@@ -441,7 +508,7 @@ def test_batch_speculative_generate_matches_reference(sd, case):
         assert rates == wrates
         return
     if ([o.cpu().tolist() for o in outs], rates) != (c["outputs"], c["rates"]):
-        tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]], pos_mult=c["pos_mult"])
+        tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]], pos_mult=c["pos_mult"], sigma=c.get("sigma", 1.0))
         octx = SimpleNamespace(drafter=dc, target=tc, gamma=c["gamma"], gen_len=c["gen_len"],
                                end_tokens=c["end_tokens"])
         torch.manual_seed(c["seed"])
@@ -520,7 +587,7 @@ def test_ngram_verify_step_matches_oracle(sd, g, V, dtype, kind, match, stop_at)
         n, xo = ref.ngram_verify_step(x, drafts, proc, noise) if g > 0 else (0, None)
         if g == 0:
             xo = int(ref.sample(ref.process(x[0:1], proc, exact), proc, noise).reshape(-1)[0])
-        stop = next((j for j in range(n) if drafts[j] in stops), -1)
+        stop = ref.stop_location(drafts[:n], stops)
         variants[exact] = (n, xo, stop, gen.get_state())
     gen2 = torch.Generator().manual_seed(5000 + seed)
     rows = [x[i:i + 1].to(DEV) for i in range(g + 1)]

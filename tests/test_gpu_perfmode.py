@@ -6,6 +6,12 @@ and the token is drawn by inverse CDF in the tail of the sampling kernel.
 * greedy rows use no noise and must equal the oracle bit for bit;
 * sampled tokens are checked in distribution (chi-square against the exact residual / p row),
   since perf mode reproduces the reference's multinomial, not torch's bit stream.
+
+Each walk runs twice: without and with the drafter rows' statistics from real sd_sample draws of the
+same rows (``draws``), as the decode loops pass them.  With them every B >= 8 call takes the one-launch
+fused verify (k_verify_fused) — the kernel behind the bench's headline — and the tests assert that
+path from sd_last_verify_path, so the fused kernel is pinned to the oracle directly, not only to the
+two-launch path (tests/test_gpu_fused.py).
 """
 from types import SimpleNamespace
 
@@ -47,13 +53,42 @@ def peaked_logits(V, n_hot, seed, dtype=torch.bfloat16):
     return x.to(dtype), hot
 
 
-def verify(sd, tl, dl, ids, rule, proc, noise, stops=(), draft_is_probs=False, **kw):
+def draft_stats(sd, dl, proc, seed=4242):
+    """(stats [γ, B, 2], keeps [γ, B, 4] or None) of the drafter rows dl [B, γ, V] as sd_sample returns
+    them with its draws (the decode loops' draft_row_stats / draft_row_keep); the drawn tokens are
+    discarded — the tests choose the drafts."""
+    B, g = dl.shape[0], dl.shape[1]
+    spec = spec_of(sd, proc)
+    stats = torch.empty(g, B, 2, device=DEV)
+    keeps = torch.empty(g, B, 4, dtype=torch.int32, device=DEV) if spec.keeps else None
+    noise = sd.PhiloxNoise(seed=seed)
+    for d in range(g):
+        sd.ops.sample_rows(dl[:, d, :].contiguous(), spec, noise, row_stats_out=stats[d],
+                           row_keep_out=keeps[d] if keeps is not None else None)
+    return stats, keeps
+
+
+def verify(sd, tl, dl, ids, rule, proc, noise, stops=(), draft_is_probs=False, draws=False, **kw):
     n_t = tl.shape[1]
     g = dl.shape[1]
-    return sd.ops.verify([tl[:, t, :] for t in range(n_t)], [dl[:, d, :] for d in range(g)], ids, rule,
-                         spec_of(sd, proc), spec_of(sd, proc), noise,
-                         torch.tensor(list(stops), dtype=torch.long, device=DEV),
-                         draft_is_probs=draft_is_probs, **kw)
+    if draws:
+        kw["draft_row_stats"], kw["draft_row_keep"] = draft_stats(sd, dl, proc)
+    out = sd.ops.verify([tl[:, t, :] for t in range(n_t)], [dl[:, d, :] for d in range(g)], ids, rule,
+                        spec_of(sd, proc), spec_of(sd, proc), noise,
+                        torch.tensor(list(stops), dtype=torch.long, device=DEV),
+                        draft_is_probs=draft_is_probs, **kw)
+    out.path = sd.lib.last_verify_path()
+    return out
+
+
+def expect_path(sd, out, B, draws, stochastic=True):
+    """With the draws' stats, B >= 8 stochastic calls take k_verify_fused, B <= 8 k_verify_lean (where
+    both apply, the lean kernel first: B == 8 bf16 plain rows)."""
+    if not draws or not stochastic:
+        return
+    assert out.path in (sd.lib.SD_PATH_VERIFY_FUSED, sd.lib.SD_PATH_VERIFY_LEAN) if B == 8 else \
+        out.path == (sd.lib.SD_PATH_VERIFY_FUSED if B > 8 else sd.lib.SD_PATH_VERIFY_LEAN), \
+        sd.lib.PATH_NAMES.get(out.path)
 
 
 def chi2_check(samples, probs, label):
@@ -108,11 +143,15 @@ def host_walk_engine(p, q, toks, ends, seed, off, b, g):
     return n, False, False, close
 
 
+@pytest.mark.parametrize("draws", [False, True], ids=["stats-in-verify", "stats-from-draws"])
 @pytest.mark.parametrize("kind,V,B,dtype", [("multi_t1", 4096, 64, torch.bfloat16),
                                             ("multi_t07", 4096, 16, torch.float32),
                                             ("topk50_t08", 8192, 16, torch.bfloat16),
-                                            ("nucleus09", 4096, 8, torch.bfloat16)])
-def test_perf_spec_accept_walk(sd, kind, V, B, dtype):
+                                            ("nucleus09", 4096, 8, torch.bfloat16),
+                                            ("multi_t1", 128256, 32, torch.bfloat16),
+                                            ("multi_t1", 50257, 8, torch.bfloat16),
+                                            ("multi_t07", 50257, 32, torch.bfloat16)])
+def test_perf_spec_accept_walk(sd, kind, V, B, dtype, draws):
     procs = {"multi_t1": ref.Processor("multinomial", 1.0), "multi_t07": ref.Processor("multinomial", 0.7),
              "topk50_t08": ref.Processor("topk", 0.8, 50), "nucleus09": ref.Processor("nucleus", 1.0, 0, 0.9)}
     proc = procs[kind]
@@ -125,7 +164,8 @@ def test_perf_spec_accept_walk(sd, kind, V, B, dtype):
     ids[: B // 2] = dl[: B // 2].float().topk(2, dim=-1).indices[..., 1]
     noise = sd.PhiloxNoise(seed=0x1234_5678_9ABC, offset=5)
     off = noise.offset
-    out = verify(sd, tl.to(DEV), dl.to(DEV), ids.to(DEV), sd.lib.SD_RULE_SPEC, proc, noise)
+    out = verify(sd, tl.to(DEV), dl.to(DEV), ids.to(DEV), sd.lib.SD_RULE_SPEC, proc, noise, draws=draws)
+    expect_path(sd, out, B, draws)
     n = out.n_accepted.cpu().tolist()
     st = out.row_status.cpu().tolist()
     kd, kt = out.prune_drafter.cpu().tolist(), out.prune_target.cpu().tolist()
@@ -155,9 +195,11 @@ def test_perf_spec_accept_walk(sd, kind, V, B, dtype):
     assert close_rows <= 1
 
 
+@pytest.mark.parametrize("draws", [False, True], ids=["stats-in-verify", "stats-from-draws"])
 @pytest.mark.parametrize("B,V,dtype", [(16, 4096, torch.bfloat16), (32, 128256, torch.bfloat16),
-                                       (8, 50257, torch.float32)])
-def test_perf_engine_accept_walk_and_state(sd, B, V, dtype):
+                                       (8, 50257, torch.float32), (8, 128256, torch.bfloat16),
+                                       (32, 50257, torch.bfloat16)])
+def test_perf_engine_accept_walk_and_state(sd, B, V, dtype, draws):
     g, step, gen_len = 4, 4, 12
     tl = rand_logits((B, g, V), dtype, 21)
     dl = (tl.float() + rand_logits((B, g, V), torch.float32, 22, 1.0)).to(dtype)
@@ -173,7 +215,9 @@ def test_perf_engine_accept_walk_and_state(sd, B, V, dtype):
     noise = sd.PhiloxNoise(seed=99, offset=1 << 33)
     off = noise.offset
     out = verify(sd, tl.to(DEV), dl.to(DEV), ids.to(DEV), sd.lib.SD_RULE_ENGINE, ref.Processor("multinomial", 1.0),
-                 noise, stops=ends, engine_state=dict(generated=gen_d, step=step, finished=fin_d, accepted=acc_d))
+                 noise, stops=ends, engine_state=dict(generated=gen_d, step=step, finished=fin_d, accepted=acc_d),
+                 draws=draws)
+    expect_path(sd, out, B, draws)
     n = out.n_accepted.cpu().tolist()
     x = out.next_token.cpu().tolist()
     st = out.row_status.cpu().tolist()
@@ -287,6 +331,52 @@ def test_perf_bonus_distribution(sd):
 
     p1 = ref.process(t1, proc, exact=True).double()
     chi2_check(_collect(sd, 4, run), p1.numpy(), "bonus")
+
+
+@pytest.mark.parametrize("case", ["residual", "bonus"])
+def test_fused_verify_distributions(sd, case):
+    """k_verify_fused's samplers (two 2048-element chunks per workgroup, the decider's chunk pick over
+    the 63 chunk totals of a V=128256 row) at the bench's B=32: the residual token of a reject at
+    slot 0 must follow (p0 - q0)+ / Σ, the bonus token of a full accept p1 — chi-square over many
+    calls (each call draws with a fresh Philox offset).  sampling/speculative_decoding.py:139-171."""
+    proc = ref.Processor("multinomial", 1.0)
+    B, V = 32, 128256
+    t0, hot = peaked_logits(V, 60, 21)
+    t1, _ = peaked_logits(V, 60, 22)
+    if case == "residual":
+        d0 = t0.float().clone()
+        d0[hot[:30]] += 1.5            # the drafter over-weights half of the hot tokens
+        d0 = d0.to(torch.bfloat16)
+        p0 = ref.process(t0, proc, exact=True).double()
+        q0 = ref.process(d0, proc, exact=True).double()
+        x = int(torch.argmax(q0 - p0))  # q >> p at the draft: most rows reject at slot 0
+        want = (p0.float() - q0.float()).clamp(min=0).double()
+        calls = 200
+    else:
+        d0 = t0                        # q == p: every draft accepted, the bonus row drawn
+        x = int(torch.argmax(t0.float()))
+        want = ref.process(t1, proc, exact=True).double()
+        calls = 160
+    tl = torch.stack([t0, t1]).unsqueeze(0).expand(B, 2, V).contiguous().to(DEV)
+    dl = d0.view(1, 1, V).expand(B, 1, V).contiguous().to(DEV)
+    ids = torch.full((B, 1), x, dtype=torch.long, device=DEV)
+    stats, _ = draft_stats(sd, dl, proc)
+    noise = sd.PhiloxNoise(seed=77)
+    xs = []
+    for _ in range(calls):
+        out = verify(sd, tl, dl, ids, sd.lib.SD_RULE_SPEC, proc, noise, draft_row_stats=stats)
+        assert out.path == sd.lib.SD_PATH_VERIFY_FUSED, sd.lib.PATH_NAMES.get(out.path)
+        flag = sd.lib.SD_ROW_RESIDUAL if case == "residual" else sd.lib.SD_ROW_BONUS
+        sel = (out.row_status & flag) != 0
+        assert not (out.row_status & sd.lib.SD_ROW_ERROR_MASK).any()
+        if case == "residual":
+            assert torch.allclose(out.resample_mass[sel].double().cpu(), want.sum().expand(int(sel.sum())), atol=1e-5)
+        else:
+            assert sel.all()
+        xs.append(out.next_token[sel].cpu().numpy())
+    samples = np.concatenate(xs)
+    assert len(samples) > 0.5 * B * calls
+    chi2_check(samples, want.numpy(), f"fused {case} V={V} B={B}")
 
 
 def test_perf_engine_fallback_distribution(sd):

@@ -1,5 +1,5 @@
 """The one-pass STREAM draw (k_draw_stream, csrc/sd_draw_stream.inc) against the oracle and the
-three-launch STREAM path (row statistics + k_rowsample + k_sample_finalize, SD_DRAW_STREAM=0).
+three-launch STREAM path (row statistics + k_rowsample + k_sample_finalize, SD_OPT_DRAW_STREAM = 0).
 
 torch.multinomial(softmax(l), 1) on [R, V] rows with the generator's words (the reference's draw,
 engine/infer_engine.py:241-246; utils/logits_processor.py:39-49) must come out bit-exact: the same
@@ -33,13 +33,17 @@ def rows(R, V, dtype, seed, kind="normal", pad=0):
 
 
 def hip_draw(x, seed, one_pass, monkeypatch):
-    from specdec_amd import ops
+    from specdec_amd import _lib, ops
     from specdec_amd.noise import StreamNoise
-    monkeypatch.setenv("SD_DRAW_STREAM", "1" if one_pass else "0")
     g = torch.Generator().manual_seed(seed)
     xd = x
     stats = torch.zeros(x.shape[0], 2, device=DEV)
-    tok, _, st = ops.sample_rows(xd, ops.PLAIN_SOFTMAX, StreamNoise(g), row_stats_out=stats)
+    with _lib.option(_lib.SD_OPT_DRAW_STREAM, 1 if one_pass else 0):
+        tok, _, st = ops.sample_rows(xd, ops.PLAIN_SOFTMAX, StreamNoise(g), row_stats_out=stats)
+    if one_pass:
+        assert _lib.last_sample_path() == _lib.SD_PATH_SAMPLE_STREAM
+    else:
+        assert _lib.last_sample_path() == _lib.SD_PATH_SAMPLE_MULTI
     torch.cuda.synchronize()
     return tok.cpu(), st.cpu(), stats.cpu(), g.get_state()
 

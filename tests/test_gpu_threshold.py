@@ -30,9 +30,10 @@ def ops():
 def thr_design(request, monkeypatch):
     """The slice maxima, tie search and radix hand-over inside k_thr_hist (polled records, the
     default when the grid is resident) or in k_thr_max / k_thr_tie launches of their own
-    (SD_THR_POLL=0); the library reads the switch on every call."""
-    monkeypatch.setenv("SD_THR_POLL", "1" if request.param == "in-launch" else "0")
-    return request.param
+    (SD_OPT_THRESHOLD_POLL = 0); the library reads the option on every call."""
+    from specdec_amd import _lib
+    with _lib.option(_lib.SD_OPT_THRESHOLD_POLL, 1 if request.param == "in-launch" else 0):
+        yield request.param
 
 
 def normal_rows(R, V, dtype, seed, scale=3.0):

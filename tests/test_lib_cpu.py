@@ -159,3 +159,54 @@ def kernel_notes(lib_path, llvm):
                                    f"--output={co}", "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"])
             out.append(subprocess.check_output([os.path.join(llvm, "llvm-readelf"), "--notes", co]).decode())
     return "\n".join(out)
+
+
+def test_dispatch_options_round_trip_and_reject_bad_values():
+    """sd_set_option / sd_get_option (ABI 10): the defaults, a scoped change, and refusals."""
+    from specdec_amd import _lib
+    defaults = {_lib.SD_OPT_FUSED_VERIFY: 1, _lib.SD_OPT_LEAN_VERIFY: -1, _lib.SD_OPT_THRESHOLD_POLL: 1,
+                _lib.SD_OPT_DRAW_STREAM: 1}
+    for o, v in defaults.items():
+        assert _lib.get_option(o) == v, o
+    with _lib.option(_lib.SD_OPT_FUSED_VERIFY, 0):
+        assert _lib.get_option(_lib.SD_OPT_FUSED_VERIFY) == 0
+    assert _lib.get_option(_lib.SD_OPT_FUSED_VERIFY) == 1
+    for o, bad in ((99, 0), (_lib.SD_OPT_FUSED_VERIFY, 3), (_lib.SD_OPT_LEAN_VERIFY, 2),
+                   (_lib.SD_OPT_THRESHOLD_POLL, -1), (_lib.SD_OPT_DRAW_STREAM, 2)):
+        assert _lib.lib.sd_set_option(o, bad) == _lib.SD_ERR_INVALID, (o, bad)
+    assert _lib.lib.sd_get_option(99, C.byref(C.c_int32())) == _lib.SD_ERR_INVALID
+    for o, v in defaults.items():
+        assert _lib.get_option(o) == v, o
+    assert _lib.last_verify_path() == _lib.SD_PATH_NONE   # nothing ran on this thread
+    assert _lib.last_sample_path() == _lib.SD_PATH_NONE
+
+
+def test_no_environment_read_on_the_call_path():
+    """The library reads the environment only for the poll policy's initial values (once, in
+    policy_init) and, in SD_PHASE_TIMING diagnostic builds, the timestamp buffer: no getenv on the
+    path of sd_verify / sd_sample / sd_ngram_verify — dispatch switches are sd_set_option."""
+    csrc = os.path.join(ROOT, "speculative-decoding_amd", "csrc")
+    found = []
+    for name in sorted(os.listdir(csrc)):
+        if not name.endswith((".hip", ".inc", ".cpp", ".h")):
+            continue
+        lines = open(os.path.join(csrc, name)).read().split("\n")
+        depth_timing = 0
+        func = None
+        for ln, line in enumerate(lines, 1):
+            s = line.strip()
+            if s.startswith("#ifdef SD_PHASE_TIMING"):
+                depth_timing += 1
+            elif s.startswith("#endif") and depth_timing:
+                depth_timing -= 1
+            m = re.match(r"^[\w:<>\s\*&]+?\b(\w+)\s*\([^;]*\)\s*\{\s*$", line)
+            if m and not line.startswith(" "):
+                func = m.group(1)
+            if "getenv(" in line:
+                found.append((name, ln, func, bool(depth_timing), re.findall(r'getenv\("(\w+)"\)', line)))
+    assert found, "scanner found no getenv at all (the poll policy's should be there)"
+    for name, ln, func, timing, vars_ in found:
+        if timing:
+            assert vars_ == ["SD_TS_PTR"], (name, ln, vars_)
+        else:
+            assert func == "policy_init" and set(vars_) <= {"SD_POLL", "SD_POLL_SPIN_LIMIT"}, (name, ln, func, vars_)

@@ -66,8 +66,8 @@ def test_ngram_loop_matches_reference(case):
 @pytest.mark.parametrize("case", sorted(ENGINE))
 def test_engine_loop_matches_reference(case):
     c = ENGINE[case]
-    target, drafter = pair(c["vocab"], c["dtype"], c["pos_mult"])
-    assert bank_digest(target) == c["target_digest"]
+    target, drafter = pair(c["vocab"], c["dtype"], c["pos_mult"], c.get("sigma", 1.0))
+    assert bank_digest(target) == c["target_digest"] and bank_digest(drafter) == c["drafter_digest"]
     ids = torch.tensor(c["prompt"], dtype=torch.long)
     ctx = SimpleNamespace(drafter=drafter, target=target, gamma=c["gamma"], gen_len=c["gen_len"],
                           end_tokens=c["end_tokens"])
