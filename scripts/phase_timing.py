@@ -98,7 +98,7 @@ for rep in range(4):
                  "finish": (wgi >= 4096) & (blk[:, 6] > 0)}
         names = {"span": {0: "start", 6: "stream_done", 1: "merged", 8: "rec_stored"},
                  "decider": {0: "start", 7: "pf_done", 9: "polled", 11: "tags_ok", 13: "reduced", 14: "ratio0", 15: "accept0", 10: "ratios", 4: "synced",
-                             5: "walked", 3: "decided"},
+                             6: "ballots", 8: "built", 12: "published", 5: "walked", 3: "decided", 1: "drec_stored"},
                  "finish": {4: "tail_S", 7: "chunk_picked", 5: "candidate", 6: "finalized"},
                  "sampler": {0: "start", 1: "saw_decision", 8: "weights", 9: "chunk_pick", 2: "done"}}
         print("fused verify roles:")

@@ -79,6 +79,21 @@ def proc_spec(proc) -> ProcSpec:
                     int(getattr(proc, "top_k", 0)), float(getattr(proc, "top_p", 1.0)))
 
 
+# sequences one Philox call verifies / samples (the arrival-counter block, kCntMax in the kernels)
+MAX_ROWS_PER_CALL = 16384
+
+
+def _row_shards(B: int, noise):
+    """Row shards of a Philox call over more than MAX_ROWS_PER_CALL sequences: [(r0, r1, noise)]
+    with ONE call offset for all shards (noise keyed by the global row = row_base + r), so the
+    shards draw what one call would.  None when the call fits (or is not Philox)."""
+    if B <= MAX_ROWS_PER_CALL or not isinstance(noise, PhiloxNoise):
+        return None
+    o = noise.next_offset()
+    return [(r0, min(B, r0 + MAX_ROWS_PER_CALL), PhiloxNoise(noise.seed, o, noise.offset_dev))
+            for r0 in range(0, B, MAX_ROWS_PER_CALL)]
+
+
 def _stream_ptr(device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
@@ -172,6 +187,14 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     R, V = logits.shape
     _require_rows(logits, "logits", V)
     dev = logits.device
+    shards = _row_shards(R, noise)
+    if shards is not None:   # more rows than one call holds: row shards, one noise offset
+        toks = tokens_out if tokens_out is not None else torch.empty(R, dtype=torch.long, device=dev)
+        outs = [sample_rows(logits[r0:r1], proc, nz, toks[r0:r1], want_prob, row_base + r0,
+                            None if row_stats_out is None else row_stats_out.view(-1, 2)[r0:r1],
+                            None if row_keep_out is None else row_keep_out.view(-1, 4)[r0:r1], status_or)
+                for r0, r1, nz in shards]
+        return (toks, torch.cat([o[1] for o in outs]) if want_prob else None, torch.cat([o[2] for o in outs]))
     tokens = tokens_out if tokens_out is not None else torch.empty(R, dtype=torch.long, device=dev)
     if tokens.dtype != torch.long or tokens.numel() < R or not tokens.is_cuda:
         raise ValueError("tokens_out must be an int64 device tensor with >= rows elements")
@@ -274,6 +297,22 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         raise ValueError(f"expected {n_t} target rows, got {len(target_rows)}")
     B, V = target_rows[0].shape
     dev = target_rows[0].device
+    shards = _row_shards(B, noise)
+    if shards is not None:   # more sequences than one call holds: row shards, one noise offset
+        outs = []
+        for r0, r1, nz in shards:
+            es = None
+            if engine_state is not None:
+                es = dict(generated=engine_state["generated"][r0:r1], step=engine_state["step"],
+                          finished=engine_state["finished"][r0:r1], accepted=engine_state["accepted"][r0:r1])
+            outs.append(verify([t[r0:r1] for t in target_rows], [d[r0:r1] for d in draft_rows], draft_tokens[r0:r1],
+                               rule, target_proc, draft_proc, nz, stop_tokens, skip_sample_adjustment, draft_is_probs,
+                               None if active is None else active[r0:r1], es, sync_noise, None, row_base + r0,
+                               None if draft_row_stats is None else draft_row_stats[:, r0:r1],
+                               None if draft_row_keep is None else draft_row_keep[:, r0:r1], status_or,
+                               None if row_counts is None else row_counts[r0:r1]))
+        cat = {f: torch.cat([getattr(o, f) for o in outs]) for f in VerifyOut.__dataclass_fields__ if f != "words_used"}
+        return VerifyOut(**cat, words_used=torch.zeros(1, dtype=torch.long, device=dev))
     tdt = target_rows[0].dtype
     # the batch stride is shared by a row set (it is irrelevant when B == 1)
     t_stride = target_rows[0].stride(0) if B > 1 else 0

@@ -486,3 +486,24 @@ def test_perf_sharded_calls_equal_one_call(sd):
     tok_a, _, _ = sd.ops.sample_rows(dl[:13, 0], spec_of(sd, proc), sd.PhiloxNoise(seed=3))
     tok_b, _, _ = sd.ops.sample_rows(dl[13:, 0], spec_of(sd, proc), sd.PhiloxNoise(seed=3), row_base=13)
     assert torch.equal(tok_all, torch.cat([tok_a, tok_b]))
+
+
+def test_batches_beyond_one_call_are_row_sharded(sd):
+    """More sequences than one Philox call holds (16384, the kernels' arrival-counter block): ops
+    splits the batch into row shards that share the call's noise offset (noise keyed by the global
+    row), so every shard equals the direct call over its rows with row_base = its first row."""
+    B, g, V = sd.ops.MAX_ROWS_PER_CALL + 40, 2, 256
+    tl = rand_logits((B, g, V), torch.bfloat16, 91).to(DEV)
+    dl = (tl.float() + rand_logits((B, g, V), torch.float32, 92, 1.0).to(DEV)).to(torch.bfloat16)
+    ids = dl.float().argmax(-1)
+    proc = ref.Processor("multinomial", 1.0)
+    out = verify(sd, tl, dl, ids, sd.lib.SD_RULE_ENGINE, proc, sd.PhiloxNoise(seed=12, offset=7))
+    assert ((out.row_status & sd.lib.SD_ROW_DONE) != 0).all()
+    lo = sd.ops.MAX_ROWS_PER_CALL - 8
+    part = verify(sd, tl[lo:], dl[lo:], ids[lo:], sd.lib.SD_RULE_ENGINE, proc, sd.PhiloxNoise(seed=12, offset=7),
+                  row_base=lo)
+    for f in ("n_accepted", "next_token", "row_status"):
+        assert torch.equal(getattr(out, f)[lo:], getattr(part, f)), f
+    tok, _, st = sd.ops.sample_rows(dl[:, 0].contiguous(), spec_of(sd, proc), sd.PhiloxNoise(seed=3))
+    tok2, _, _ = sd.ops.sample_rows(dl[lo:, 0].contiguous(), spec_of(sd, proc), sd.PhiloxNoise(seed=3), row_base=lo)
+    assert torch.equal(tok[lo:], tok2) and (st & sd.lib.SD_ROW_DONE).all()
