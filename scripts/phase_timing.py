@@ -8,7 +8,7 @@ start / reach each phase relative to the kernel's first start (µs, s_memrealtim
 import os
 import sys
 
-os.environ["SPECDEC_LIB"] = "libspecdec_ts.so"
+os.environ.setdefault("SPECDEC_LIB", "libspecdec_ts.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "speculative-decoding_amd")]
 

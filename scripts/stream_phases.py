@@ -6,7 +6,7 @@ rows of 128256 bf16.  k_rowsample phases: 0 start, 1 logits + words + row stats 
 import os
 import sys
 
-os.environ["SPECDEC_LIB"] = "libspecdec_ts.so"
+os.environ.setdefault("SPECDEC_LIB", "libspecdec_ts.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "speculative-decoding_amd"), ROOT]
 

@@ -7,7 +7,7 @@ Prints when the row's slice workgroups reach each phase, µs after the first sta
 import os
 import sys
 
-os.environ["SPECDEC_LIB"] = "libspecdec_ts.so"
+os.environ.setdefault("SPECDEC_LIB", "libspecdec_ts.so")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [os.path.join(ROOT, "speculative-decoding_amd")]
 

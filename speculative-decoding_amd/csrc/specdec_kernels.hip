@@ -1042,6 +1042,14 @@ __device__ __forceinline__ void draft_ratio(const Plan& P, int b, int i, const D
         return;
     }
     const int rt = b * P.slots + i;
+    if constexpr (DT >= 0) {   // both rows of dtype DT, drafter logits (the fused / lean launches)
+        const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
+        p = round_dt<DT>(sd_exp(process_value<DT>(pf.xt, pf.tok, P.tT, P.t_keep, kt) - mst.x) / mst.y);
+        const int rd = b * P.slots + P.n_tslots + i;
+        const RowKeep kd = P.d_keep ? keep_of(P, rd) : RowKeep{-INFINITY, INT_MAX, 0, 0};
+        q = round_dt<DT>(sd_exp(process_value<DT>(pf.xd, pf.tok, P.dT, P.d_keep, kd) - msd.x) / msd.y);
+        return;
+    }
     const RowKeep kt = P.t_keep ? keep_of(P, rt) : RowKeep{-INFINITY, INT_MAX, 0, 0};
     const float yt = P.tdt == SD_BF16 ? process_value<SD_BF16>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
                    : P.tdt == SD_F32 ? process_value<SD_F32>(pf.xt, pf.tok, P.tT, P.t_keep, kt)
