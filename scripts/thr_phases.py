@@ -35,7 +35,8 @@ PH = {0: "start", 1: "max_pub", 2: "loc_hist", 3: "max_exch", 4: "tail", 5: "tai
       7: "arrived", 8: "hist_read", 9: "norm_scan", 10: "mass_scan", 11: "decided", 12: "decision", 13: "tie_rec",
       14: "keep_out"}
 if NUC:
-    PH = {0: "start", 1: "max", 2: "s1+prefix", 3: "picks", 4: "B_recs", 5: "C_sums", 6: "D_recs"}
+    PH = {0: "start", 1: "max", 2: "s1+prefix", 3: "picks", 7: "B_polled", 4: "B_recs", 5: "C_sums", 8: "D_polled",
+          6: "D_recs"}
 for rep in range(4):
     ts.zero_()
     torch.cuda.synchronize()
