@@ -936,67 +936,120 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
         __shared__ float lrp[kWalkDrafts], lrq[kWalkDrafts];
         __shared__ uint8_t lstop[kWalkDrafts], lact[kWalkDrafts];
         __shared__ int32_t la[kWalkDrafts], lk[kWalkDrafts];
+        __shared__ uint64_t lstpm[kWalkDrafts];   // row bi: bit i = draft i is a stop token
         __shared__ int64_t s_off;
+        __shared__ int64_t s_stops[kLdsStops];
         const int tid = threadIdx.x, lane = tid & 63, g = P.gamma;
         const int64_t V2 = 2ll * P.V;
         const bool spec = P.rule == SD_RULE_SPEC;
         int nbmax = 1;
         while ((nbmax + 1) * (nbmax + 1) * g <= kWalkWords && (nbmax + 1) * g <= kWalkDrafts) ++nbmax;
         if (tid == 0) s_off = 0;
+        const bool lds_stops = P.n_stop <= kLdsStops;
+        if (lds_stops && tid < P.n_stop) s_stops[tid] = P.stops[tid];
         SD_TS(8000, 0);
         __syncthreads();
         for (int b0 = 0; b0 < P.B; b0 += nbmax) {
             const int nb = min(nbmax, P.B - b0), W = nb * g;
             const int64_t off = s_off;
-            {   // every load in flight before the first LDS write (a loop of load -> store pairs waited
-                // for each load in turn: ~16 dependent round trips)
+            {   // every load of the block in flight at once — the windows' words (window k, word j at
+                // lw[k W + j]; the window index by an exact fp32 reciprocal, not an integer division
+                // per load), the drafts' p/q, ids and the rows' active flags — then the LDS writes
+                // (a load behind a per-load branch, or a loop of load -> store pairs, paid one round
+                // trip each)
                 constexpr int kPer = kWalkWords / 256;
+                const float invW = 1.0f / (float)W;
+                const int nw = nb * W;
                 uint32_t wv[kPer];
 #pragma unroll
                 for (int q = 0; q < kPer; ++q) {
                     const int i = tid + q * 256;
-                    const int k = i / W, j = i - k * W;
+                    const int k = (int)(((float)i + 0.5f) * invW), j = i - k * W;   // exact: i, W < 2^14
                     const int64_t w = off + V2 * k + j;
-                    wv[q] = i < nb * W && w < P.noise.n_words ? P.noise.words[w] : 0u;
+                    const bool ok = i < nw && w < P.noise.n_words;
+                    wv[q] = P.noise.words[ok ? w : 0];
+                    wv[q] = ok ? wv[q] : 0u;
+                }
+                constexpr int kPerD = kWalkDrafts / 256;
+                float rp[kPerD], rq[kPerD];
+                int64_t tok[kPerD];
+                int32_t act[kPerD];
+#pragma unroll
+                for (int q = 0; q < kPerD; ++q) {
+                    const int i = tid + q * 256;
+                    const int bi = i / g, d = i - bi * g, b = b0 + (i < W ? bi : 0);
+                    const int e = b * g + (i < W ? d : 0);
+                    rp[q] = P.rp[e];
+                    rq[q] = P.rq[e];
+                    tok[q] = P.draft_tokens[b * P.tok_stride + (i < W ? d : 0)];
+                    act[q] = P.active == nullptr ? 1 : P.active[b] != 0;
                 }
 #pragma unroll
                 for (int q = 0; q < kPer; ++q)
-                    if (tid + q * 256 < nb * W) lw[tid + q * 256] = wv[q];
+                    if (tid + q * 256 < nw) lw[tid + q * 256] = wv[q];
+#pragma unroll
+                for (int q = 0; q < kPerD; ++q) {
+                    const int i = tid + q * 256;
+                    if (i >= W) continue;
+                    const float p = rp[q], qq = rq[q];
+                    lrp[i] = p;
+                    lrq[i] = qq;
+                    // accept iff u <= p/q (fp32, SPEC) / u < min(1, p/q) (fp64, ENGINE): accept_draft's rules
+                    lthr[i] = spec ? (double)(p / qq) : ((double)qq <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)qq));
+                    uint32_t r8 = 0;   // stop_rank8 from the staged list
+                    if (lds_stops) {
+                        for (int k = P.n_stop - 1; k >= 0; --k)
+                            if (s_stops[k] == tok[q]) r8 = k < 254 ? (uint32_t)k + 1u : 255u;
+                    } else {
+                        r8 = stop_rank8(P, tok[q]);
+                    }
+                    lstop[i] = (uint8_t)r8;
+                    lact[i] = (uint8_t)act[q];
+                }
             }
-            for (int i = tid; i < W; i += blockDim.x) {
-                const int b = b0 + i / g, d = i - (i / g) * g;
-                const float p = P.rp[b * g + d], q = P.rq[b * g + d];
-                lrp[i] = p;
-                lrq[i] = q;
-                // accept iff u <= p/q (fp32, SPEC) / u < min(1, p/q) (fp64, ENGINE): accept_draft's rules
-                lthr[i] = spec ? (double)(p / q) : ((double)q <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)q));
-                lstop[i] = stop_rank8(P, P.draft_tokens[b * P.tok_stride + d]);
-                lact[i] = P.active == nullptr || P.active[b] != 0;
+            __syncthreads();
+            for (int bi = tid; bi < nb; bi += blockDim.x) {   // the rows' stop masks (off the chain)
+                uint64_t m = 0;
+                for (int i = 0; i < g; ++i) m |= lstop[bi * g + i] != 0 ? 1ull << i : 0ull;
+                lstpm[bi] = m;
             }
             __syncthreads();
             SD_TS(8000, 1);
-            if (tid < kWave) {   // the chain: (a, k) of every row
-                int a = 0, k = 0;
+            if (tid < kWave) {   // the chain: (a, k) of every row; per row only the uniforms' LDS read
+                // depends on the previous row — the next row's threshold / flags are loaded during
+                // this one, and rows < 64 keep their (a, k) in lane bi's registers (no LDS write on
+                // the chain)
+                int a = 0, k = 0, my_a = 0, my_k = 0;
                 const bool in = lane < g;
+                double t = lthr[in ? lane : 0];
+                uint64_t stp = lstpm[0];
+                bool ract = lact[0] != 0;
                 for (int bi = 0; bi < nb; ++bi) {
-                    if (lane == 0) { la[bi] = a; lk[bi] = k; }
-                    const int e = bi * g + (in ? lane : 0);
                     const float u = uniform_from_word(lw[k * W + a + (in ? lane : 0)]);
-                    const double t = lthr[e];
+                    const int bn = bi + 1 < nb ? bi + 1 : bi;
+                    const double t_n = lthr[bn * g + (in ? lane : 0)];
+                    const uint64_t stp_n = lstpm[bn];
+                    const bool ract_n = lact[bn * g] != 0;
+                    if (lane == (bi & 63)) { my_a = a; my_k = k; }
+                    if (bi >= kWave && lane == 0) { la[bi] = a; lk[bi] = k; }
                     const bool acc = spec ? !((double)u > t) : (double)u < t;
-                    const uint64_t rej = __ballot(in && !acc), stp = __ballot(in && lstop[e] != 0);
+                    const uint64_t rej = __ballot(in && !acc);
                     const int f = rej ? __builtin_ctzll(rej) : g;              // first rejected draft
                     const uint64_t before = f >= 64 ? ~0ull : ((1ull << f) - 1ull);
                     const uint64_t stop_acc = stp & before;
                     if (spec) {
                         a += g;
                         k += (P.t_stoch && !stop_acc) ? 1 : 0;
-                    } else if (lact[bi * g] != 0) {
+                    } else if (ract) {
                         if (stop_acc) a += __builtin_ctzll(stop_acc) + 1;      // finished on an end token
                         else if (f < g) { a += f + 1; k += 1; }                  // rejected: the residual row
                         else a += g;
                     }
+                    t = t_n;
+                    stp = stp_n;
+                    ract = ract_n;
                 }
+                if (lane < nb) { la[lane] = my_a; lk[lane] = my_k; }
                 if (lane == 0) s_off = off + a + V2 * k;
             }
             __syncthreads();
