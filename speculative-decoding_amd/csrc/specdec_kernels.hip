@@ -26,6 +26,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <map>
+#include <tuple>
 #include <atomic>
 #include <mutex>
 #include <type_traits>
@@ -3679,20 +3680,23 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
         {{sd::k_verify_lean<SD_F16, false, false>, sd::k_verify_lean<SD_F16, false, true>},
          {sd::k_verify_lean<SD_F16, true, false>, sd::k_verify_lean<SD_F16, true, true>}}};
     const K kern = kerns[di][fast][stoch];
+    // the staged spans: the target rows and the drafter rows the launch loads, 4 KB each
+    const int nload = P0.n_tslots + ((stoch || !P0.dstats) ? P0.gamma : 0);
+    const size_t dyn = (size_t)nload * kThreads * sizeof(uint4);
     static std::mutex mu;
-    static std::map<std::pair<int, const void*>, int> caps;
+    static std::map<std::tuple<int, const void*, size_t>, int> caps;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) { lean_why(10); return 0; }
     int cap;
     {
         std::lock_guard<std::mutex> lk(mu);
-        auto it = caps.find({dev, (const void*)kern});
+        auto it = caps.find({dev, (const void*)kern, dyn});
         if (it == caps.end()) {
             int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, sd::kLeanThreads, 0) != hipSuccess ||
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kern, sd::kLeanThreads, dyn) != hipSuccess ||
                 hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
                 per_cu = cus = 0;
-            it = caps.emplace(std::make_pair(dev, (const void*)kern), per_cu * cus).first;
+            it = caps.emplace(std::make_tuple(dev, (const void*)kern, dyn), per_cu * cus).first;
         }
         cap = it->second;
     }
@@ -3710,7 +3714,8 @@ int32_t launch_verify_lean(const sd::Plan& P0, void* stream) {
     // both fit the workspace's rpart region: B (2γ+1) (nc+1) ResParts >= B n_span (ResPart + 16 (2γ+1))
     const uintptr_t srec = reinterpret_cast<uintptr_t>(P0.rpart + (int64_t)P0.B * n_span);
     P.srec = reinterpret_cast<uint4*>((srec + 15) & ~uintptr_t(15));
-    SD_LAUNCH(kern, dim3(n_span, P.B), dim3(sd::kLeanThreads), stream, P);
+    hipLaunchKernelGGL(kern, dim3(n_span, P.B), dim3(sd::kLeanThreads), (unsigned)dyn, (hipStream_t)stream, P);
+    if (const hipError_t e = hipGetLastError(); e != hipSuccess) { g_last_error = e; return SD_ERR_LAUNCH; }
     lean_why(0);
     return 1;
 }
