@@ -2,7 +2,8 @@
 
 Loads the SD_PHASE_TIMING build (make -C speculative-decoding_amd timing), runs the bench
 shape (engine rule, B=32, γ=4, V=128256 bf16, Philox; B=1 RULE=spec: configs[1]'s multinomial
-verify over γ+1 target rows) and prints, per kernel, when workgroups
+verify over γ+1 target rows; PROC=nucleus: configs[1]'s nucleus-0.9 verify, the drafter rows'
+statistics reduced in the launch as the drop-in loop does for nucleus drafters) and prints, per kernel, when workgroups
 start / reach each phase relative to the kernel's first start (µs, s_memrealtime = 100 MHz).
 """
 import os
@@ -28,9 +29,11 @@ tl = (torch.randn(B, NT, V, device=dev, generator=g) * 3).to(torch.bfloat16)
 dl = (tl[:, :G].float() + torch.randn(B, G, V, device=dev, generator=g)).to(torch.bfloat16)
 ids = dl.float().argmax(-1)
 noise = PhiloxNoise(seed=1)
+NUC = os.environ.get("PROC") == "nucleus"
+proc = ops.ProcSpec("nucleus", 1.0, 0, 0.9) if NUC else ops.PLAIN_SOFTMAX
 # the bench's verify: drafter rows' (max, Σexp) come from the draws, k_stats reads target rows only
-dstats = torch.empty(G, B, 2, device=dev)
-for d in range(G):
+dstats = None if NUC else torch.empty(G, B, 2, device=dev)
+for d in range(G if not NUC else 0):
     ops.sample_rows(dl[:, d], ops.PLAIN_SOFTMAX, noise, row_stats_out=dstats[d])
 ts = torch.zeros(16384 * 16, dtype=torch.int64, device=dev)
 
@@ -38,7 +41,7 @@ ts = torch.zeros(16384 * 16, dtype=torch.int64, device=dev)
 def step():
     return ops.verify([tl[:, t] for t in range(NT)], [dl[:, t] for t in range(G)], ids,
                       _lib.SD_RULE_SPEC if SPEC else _lib.SD_RULE_ENGINE,
-                      ops.PLAIN_SOFTMAX, ops.PLAIN_SOFTMAX, noise, torch.tensor([], dtype=torch.long, device=dev),
+                      proc, proc, noise, torch.tensor([], dtype=torch.long, device=dev),
                       draft_row_stats=dstats)
 
 

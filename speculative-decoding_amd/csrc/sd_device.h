@@ -450,6 +450,15 @@ __device__ __forceinline__ float wave_incl_scan(float v) {
     v += dpp_f<kDppRowBcast31, 0xC>(0.f, v);
     return v;
 }
+__device__ __forceinline__ int wave_incl_scan_i(int v) {   // integer inclusive scan (lane order)
+    v += dpp_i<kDppRowShr1, 0xF, true>(0, v);
+    v += dpp_i<kDppRowShr2, 0xF, true>(0, v);
+    v += dpp_i<kDppRowShr4, 0xF, true>(0, v);
+    v += dpp_i<kDppRowShr8, 0xF, true>(0, v);
+    v += dpp_i<kDppRowBcast15, 0xA>(0, v);
+    v += dpp_i<kDppRowBcast31, 0xC>(0, v);
+    return v;
+}
 __device__ __forceinline__ double wave_incl_scan_d(double v) {
     v += dpp_d<kDppRowShr1, 0xF, true>(0.0, v);
     v += dpp_d<kDppRowShr2, 0xF, true>(0.0, v);

@@ -119,6 +119,7 @@ struct Plan {
     uint32_t* thr_part;   // 16-bit thresholds (sd_threshold.inc): per (row, slice) max key | NaN-inf flag
     float* thr_tail;      //   per (row, slice) Σexp below the window / tie counts
     int32_t* thr_hist;    //   per-row key histogram (global atomics)
+    int32_t* thr_shist;   //   poll mode: every (row, slice)'s own histogram window (the decider's tie counts)
     struct ThrRow* thr;   //   per-row tie request
     uint32_t* cnt;        // per-sequence arrival counters (seq_counter): set 0 k_stats, set 1 k_sample
     uint64_t* ts;         // SD_PHASE_TIMING builds only: per-workgroup phase timestamps
@@ -3393,6 +3394,7 @@ void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     P.thr_part = c.take<uint32_t>((size_t)rows_total * kThrMaxSlices);
     P.thr_tail = c.take<float>((size_t)rows_total * kThrMaxSlices);
     P.thr_hist = c.take<int32_t>((size_t)rows_total * kThrWin);
+    P.thr_shist = c.take<int32_t>((size_t)kThrShistSlots * kThrWin);
     P.thr = c.take<ThrRow>(rows_total);
 }
 
