@@ -354,6 +354,21 @@ __device__ __forceinline__ float process_value(float x, int64_t j, float T, bool
     return v;
 }
 
+// process_value over N consecutive elements (indices e0 ..): the keep mask and NaN rule per element,
+// then the temperature behind ONE wave-uniform branch — the same values as N process_value calls
+// (a masked value divided by T either way; NaN / T stays NaN), without a branch per element
+template <int DT, int N>
+__device__ __forceinline__ void process_vec(float* x, int64_t e0, float T, bool has_keep, const RowKeep& keep) {
+    if (has_keep) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) x[k] = process_value<DT>(x[k], e0 + k, 1.0f, true, keep);
+    }
+    if (T != 1.0f) {
+#pragma unroll
+        for (int k = 0; k < N; ++k) x[k] = round_dt<DT>(x[k] / T);
+    }
+}
+
 // ---------------------------------------------------------------- wave primitives (DPP)
 // Cross-lane steps use DPP lane shuffles (a VALU operand modifier, a few cycles) instead of
 // __shfl (ds_bpermute through the LDS crossbar, ~100 cycles per dependent step).  Reductions:

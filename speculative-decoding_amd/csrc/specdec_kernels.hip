@@ -539,9 +539,11 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     auto consume = [&](const float* x, int64_t e0, auto checked) {
         float y[VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            y[k] = FAST ? x[k] : process_value<DT>(x[k], e0 + k, T, has_keep, kp);
-            if constexpr (decltype(checked)::value) y[k] = e0 + k < hi ? y[k] : -INFINITY;
+        for (int k = 0; k < VEC; ++k) y[k] = x[k];
+        if constexpr (!FAST) process_vec<DT, VEC>(y, e0, T, has_keep, kp);
+        if constexpr (decltype(checked)::value) {
+#pragma unroll
+            for (int k = 0; k < VEC; ++k) y[k] = e0 + k < hi ? y[k] : -INFINITY;
         }
         float sv = 0.f;
 #pragma unroll
@@ -1439,16 +1441,20 @@ __device__ __forceinline__ void resid_body(const Plan& P, const Decision& d, int
         } else {
             if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
         }
+        if constexpr (!FAST) {
+            process_vec<TDT, VEC>(xt, e0, P.tT, P.t_keep, kt);
+            if (!P.draft_is_probs) process_vec<DDT, VEC>(xd, e0, P.dT, P.d_keep, kd);
+        }
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
-            const float yt = FAST ? xt[k] : process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt);
+            const float yt = xt[k];
             const float p = prob_exact<TDT>(yt, mst.x, mst.y, t_inv);
             float q;
             if (P.draft_is_probs) {
                 q = xd[k];
             } else {
-                const float yd = FAST ? xd[k] : process_value<DDT>(xd[k], j, P.dT, P.d_keep, kd);
+                const float yd = xd[k];
                 q = prob_exact<DDT>(yd, msd.x, msd.y, d_inv);
             }
             const float diff = p - q;                                 // bf16/fp32 - fp32 -> fp32
@@ -1559,12 +1565,12 @@ __device__ __forceinline__ void prow_body(const Plan& P, const Decision& d, int 
         float xt[VEC], e[VEC];
         load_vec<TDT>(trow, e0, P.V, t_al, xt);
         if (stoch) exp_noise_vec<VEC, NZ>(P.noise, d.noise_off, b, e0, P.V, e);
+        if constexpr (!FAST) process_vec<TDT, VEC>(xt, e0, P.tT, P.t_keep, kt);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = prob_exact<TDT>(FAST ? xt[k] : process_value<TDT>(xt[k], j, P.tT, P.t_keep, kt),
-                                            mst.x, mst.y, t_inv);
+            const float p = prob_exact<TDT>(xt[k], mst.x, mst.y, t_inv);
             float val = p;
             if (stoch) {   // multinomial: round_dt(p / round_dt(E))
                 const float eb = round_dt<TDT>(e[k]);
@@ -1837,10 +1843,17 @@ template <int TDT, int DDT, bool FAST>
 __device__ __forceinline__ void pair_weights_from(const PairRows& R, int64_t e0, const float* xt, const float* xd,
                                                   float* w, float* pw) {
     constexpr int VEC = PairVec<TDT, DDT>::kVec;
+    float yt_v[VEC], yd_v[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) { yt_v[k] = xt[k]; yd_v[k] = R.resid ? xd[k] : 0.f; }
+    if constexpr (!FAST) {
+        process_vec<TDT, VEC>(yt_v, e0, R.tT, R.t_keep, R.kt);
+        if (R.resid && !R.dprobs) process_vec<DDT, VEC>(yd_v, e0, R.dT, R.d_keep, R.kd);
+    }
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
         const int64_t j = e0 + k;
-        const float yt = FAST ? xt[k] : process_value<TDT>(xt[k], j, R.tT, R.t_keep, R.kt);
+        const float yt = yt_v[k];
         const float p = prob_fast<TDT>(yt, R.mst.x, R.t_inv);
         float v = p;
         if (R.resid) {
@@ -1848,8 +1861,7 @@ __device__ __forceinline__ void pair_weights_from(const PairRows& R, int64_t e0,
             if (R.dprobs) {
                 q = xd[k];
             } else {
-                const float yd = FAST ? xd[k] : process_value<DDT>(xd[k], j, R.dT, R.d_keep, R.kd);
-                q = prob_fast<DDT>(yd, R.msd.x, R.d_inv);
+                q = prob_fast<DDT>(yd_v[k], R.msd.x, R.d_inv);
             }
             const float diff = p - q;
             v = diff > 0.f ? diff : 0.f;
@@ -2540,11 +2552,12 @@ __device__ void rowsample_body(const Plan& P, int r, int c) {
         float x[VEC], e[VEC];
         load_vec<DT>(row, e0, P.V, al, x);
         if (P.t_stoch) exp_noise_vec<VEC, NZ>(P.noise, woff, r, e0, P.V, e);
+        process_vec<DT, VEC>(x, e0, P.tT, P.t_keep, kp);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = prob_exact<DT>(process_value<DT>(x[k], j, P.tT, P.t_keep, kp), ms.x, ms.y, inv_s);
+            const float p = prob_exact<DT>(x[k], ms.x, ms.y, inv_s);
             float val = p;
             if (P.t_stoch) {
                 const float eb = round_dt<DT>(e[k]);
@@ -2680,11 +2693,12 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_draw(Plan P) {
         if (T != T) PT = 1.f;   // NaN / +inf in the span: the general path's flag
     } else {
     auto take = [&](int v, int64_t e0, const float* x) {
+        float yv[VEC];
 #pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-            const float yk = FAST ? x[k] : process_value<DT>(x[k], e0 + k, P.tT, P.t_keep, kp);
-            y[v * VEC + k] = e0 + k < P.V ? yk : -INFINITY;
-        }
+        for (int k = 0; k < VEC; ++k) yv[k] = x[k];
+        if constexpr (!FAST) process_vec<DT, VEC>(yv, e0, P.tT, P.t_keep, kp);
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) y[v * VEC + k] = e0 + k < P.V ? yv[k] : -INFINITY;
     };
     if (al && P.V >= VEC) {   // every stage's vector in flight at once (ld16_clamped)
         const int64_t last = last_whole_vec<DT>(P.V);
@@ -3276,11 +3290,12 @@ __device__ void writeprobs_body(const Plan& P, void* out, int64_t ostride, int r
         const int64_t e0 = base + ((int64_t)v * kThreads + threadIdx.x) * VEC;
         float x[VEC];
         load_vec<DT>(row, e0, P.V, al, x);
+        process_vec<DT, VEC>(x, e0, P.tT, P.t_keep, kp);
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
             const int64_t j = e0 + k;
             if (j >= P.V) continue;
-            const float p = round_dt<DT>(sd_exp(process_value<DT>(x[k], j, P.tT, P.t_keep, kp) - ms.x) / ms.y);
+            const float p = round_dt<DT>(sd_exp(x[k] - ms.x) / ms.y);
             if constexpr (DT == SD_F32) reinterpret_cast<float*>(orow)[j] = p;
             else if constexpr (DT == SD_BF16) reinterpret_cast<uint16_t*>(orow)[j] = (uint16_t)(__float_as_uint(p) >> 16);
             else reinterpret_cast<__half*>(orow)[j] = __float2half_rn(p);
