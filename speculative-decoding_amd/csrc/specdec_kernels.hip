@@ -128,6 +128,7 @@ struct Plan {
     int32_t spoll;       // k_sample (stochastic tails): poll-mode finish (tagged chunk records, no counter)
     int32_t kpoll;        // k_stats (decide tail): poll-mode partials (tagged records, no counter)
     int32_t thr_poll;     // k_thr_hist: slice maxima exchanged in-launch (no k_thr_max launch)
+    uint32_t call_nonce;  // sd_verify: per-call value mixed into the sequence epoch (seq_epoch)
     int32_t spin_limit;   // poll modes: re-reads before a record counts as lost (sd_set_poll_policy)
     int32_t* status_or;   // caller's sticky error word (nullable): every row's SD_ROW_ERROR_MASK bits
     int64_t* row_counts;  // sd_verify (nullable): per row += (accepted n, tokens emitted)
@@ -167,6 +168,17 @@ constexpr int32_t kLostDecision = -2;   // fused verify: a sampler's record when
 constexpr int kCntStride = 32;   // uint32 words per counter (128 B)
 __device__ __forceinline__ uint32_t* seq_counter(const uint32_t* base, int set, int b) {
     return const_cast<uint32_t*>(base) + ((size_t)set * kCntMax + b) * kCntStride;
+}
+// This call's epoch of sequence b (counter set 3), mixed with the call's nonce: a workgroup of an
+// earlier call dispatched only after that call's waits gave up (and its epoch moved on) tags its
+// records with the earlier nonce, so the next call never takes them as its own.  The counter itself
+// only counts up (seq_advance unmixes before the +1), so the replays of a captured graph, which
+// share one nonce, never see an epoch again.
+__device__ __forceinline__ uint32_t seq_epoch(const Plan& P, int b) {
+    return __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ^ P.call_nonce;
+}
+__device__ __forceinline__ void seq_advance(const Plan& P, int b, uint32_t epoch) {
+    __hip_atomic_store(seq_counter(P.cnt, 3, b), (epoch ^ P.call_nonce) + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ const void* row_ptr(const Plan& P, int r, int* dt, float* T, bool* keep) {
@@ -469,7 +481,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
         DraftPf pf;
         const int pi = pf_draft(P);
         pf_early(P, b, pi, pf);
-        if (threadIdx.x == 0) s_epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) s_epoch = seq_epoch(P, b);
         pf_late(P, b, pi, pf);
         __syncthreads();
         SD_TS(wg_id, 7);
@@ -485,7 +497,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
             SD_TS(wg_id, 3);
         }
         if (threadIdx.x == 0)   // every span has read the epoch (its record carries it): advance it
-            __hip_atomic_store(seq_counter(P.cnt, 3, b), s_epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            seq_advance(P, b, s_epoch);
         return;
     }
     const bool is_t = s < nt;
@@ -500,7 +512,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     uint32_t ep_reg = 0u;
     bool ep_read = false;
     auto read_epoch = [&]() {
-        if (ep_thread && !ep_read) ep_reg = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (ep_thread && !ep_read) ep_reg = seq_epoch(P, b);
         ep_read = true;
     };
     // TAIL, counter mode: drafted ids now (consumed after the loop), their logits right after it,
@@ -2192,7 +2204,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
     // poll mode (stochastic tails): this call's epoch of sequence b, read beside the decision load
     const bool poll = STOCH && P.spoll;
     uint32_t epoch = 0;
-    if (poll) epoch = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (poll) epoch = seq_epoch(P, b);
     PairRows R{};
     if (d.mode != kModeNone) {
         if constexpr (STOCH) {
@@ -2219,7 +2231,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
             __syncthreads();
             sample_finish<TDT, DDT, FAST, STOCH>(P, d, b, R, u_row, wg_id, &s_epoch);
             if (threadIdx.x == 0)
-                __hip_atomic_store(seq_counter(P.cnt, 3, b), epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                seq_advance(P, b, epoch);
             return;
         }
         __shared__ int s_last;
@@ -2333,7 +2345,7 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
         uint32_t ep = 0;
-        if (lane == 0) ep = __hip_atomic_load(seq_counter(P.cnt, 3, b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) ep = seq_epoch(P, b);
         ep = __builtin_amdgcn_readfirstlane(ep);
         bool have = lane >= 2;
         uint4 r = make_uint4(0u, 0u, 0u, 0u);
@@ -3963,6 +3975,8 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
 
     g_verify_path = SD_PATH_NONE;
     Plan P{};
+    static std::atomic<uint32_t> call_seq{0};
+    P.call_nonce = 0x9E3779B9u * (call_seq.fetch_add(1, std::memory_order_relaxed) + 1u);
     P.B = a->batch; P.gamma = a->gamma; P.V = a->vocab; P.rule = a->rule;
     P.n_tslots = n_t;
     P.n_dslots = a->draft_is_probs ? 0 : a->gamma;

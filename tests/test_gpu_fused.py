@@ -109,7 +109,17 @@ def test_fused_verify_polls_are_bounded():
             set_poll_policy(*old)
 
     with fused(1):
+        ref = run(tl, dl, "engine", spec, 5)
         a = run(tl, dl, "engine", spec, 5, verify_ctx=no_polls)
+        # the next calls on the same workspace are healthy: nothing the timed-out call left behind (its
+        # records, its samplers, its epoch) is taken as theirs — no flags, the same outputs as before
+        b = run(tl, dl, "engine", spec, 5)
+        c = run(tl, dl, "engine", spec, 5)
     assert int(a["path"]) == _lib.SD_PATH_VERIFY_FUSED
     assert (a["row_status"] & _lib.SD_ROW_EXCHANGE_TIMEOUT).all()
     assert (a["row_status"] & _lib.SD_ROW_INVALID_DIST).all()
+    for o in (b, c):
+        assert int(o["path"]) == _lib.SD_PATH_VERIFY_FUSED
+        assert not (o["row_status"] & (_lib.SD_ROW_EXCHANGE_TIMEOUT | _lib.SD_ROW_INVALID_DIST)).any()
+        for k in ("n_accepted", "next_token", "row_status"):
+            assert torch.equal(o[k], ref[k]), k
