@@ -342,7 +342,7 @@ struct ProcParams {
 template <int DT>
 __device__ __forceinline__ float process_value(float x, int64_t j, float T, bool has_keep, const RowKeep& keep) {
     float v = x;
-    if (has_keep && !(x > keep.tau || (x == keep.tau && j <= keep.tie_idx))) v = round_dt<DT>(kNegFill);
+    if (has_keep && !(x > keep.tau || (x == keep.tau && (int32_t)j <= keep.tie_idx))) v = round_dt<DT>(kNegFill);   // j < 2^31
     if (T != 1.0f) v = round_dt<DT>(v / T);
     // A NaN / +inf logit under a top-k / nucleus keep stays NaN whether the cut keeps it or not:
     // torch's topk and sort rank NaN first and keep +inf, whose softmax is NaN (inf - inf), so the
@@ -357,12 +357,23 @@ __device__ __forceinline__ float process_value(float x, int64_t j, float T, bool
 // process_value over N consecutive elements (indices e0 ..): the keep mask and NaN rule per element,
 // then the temperature behind ONE wave-uniform branch — the same values as N process_value calls
 // (a masked value divided by T either way; NaN / T stays NaN), without a branch per element
+// The keep mask and NaN rule of process_value over N consecutive elements (indices e0 ..): the tie
+// index compare becomes one 32-bit compare against a per-vector constant (element k is an allowed
+// tie iff k <= tie_idx - e0; indices are < 2^31)
+template <int DT, int N>
+__device__ __forceinline__ void keep_vec(float* x, int64_t e0, const RowKeep& keep) {
+    const int32_t jr = keep.tie_idx - (int32_t)e0;
+    const float fill = round_dt<DT>(kNegFill);
+#pragma unroll
+    for (int k = 0; k < N; ++k) {
+        const float xv = x[k];
+        const float v = (xv > keep.tau || (xv == keep.tau && k <= jr)) ? xv : fill;
+        x[k] = xv <= 3.402823466e38f ? v : __builtin_nanf("");
+    }
+}
 template <int DT, int N>
 __device__ __forceinline__ void process_vec(float* x, int64_t e0, float T, bool has_keep, const RowKeep& keep) {
-    if (has_keep) {
-#pragma unroll
-        for (int k = 0; k < N; ++k) x[k] = process_value<DT>(x[k], e0 + k, 1.0f, true, keep);
-    }
+    if (has_keep) keep_vec<DT, N>(x, e0, keep);
     if (T != 1.0f) {
 #pragma unroll
         for (int k = 0; k < N; ++k) x[k] = round_dt<DT>(x[k] / T);
