@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--stream-steps", type=int, default=5, help="STREAM-mode (bit-exact noise) steps; 0 = skip")
     ap.add_argument("--no-configs1", action="store_true", help="skip the configs[1] / configs[4] batch-1 lines")
     ap.add_argument("--no-shards", action="store_true", help="skip the 16 / 8 / 4-row shard lines")
+    ap.add_argument("--sweep-batches", default="128,512",
+                    help="rows per GPU of the large-batch roofline sweep (SURVEY §8(d)); empty = skip")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the end-to-end line (random-init Llama-3-8B / 3.2-1B shaped models, drop-in engine)")
     ap.add_argument("--e2e-gen", type=int, default=64, help="new tokens per row in the end-to-end line")
@@ -79,9 +81,11 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL, one GPU per rank) or gloo (rehearsing N ranks on fewer GPUs)")
     a = ap.parse_args()
+    a.sweep_batches = [int(x) for x in a.sweep_batches.split(",") if x.strip()]
     if a.profile_only:
         a.no_cpu_baseline = a.no_configs1 = a.no_shards = a.no_e2e = True
         a.stream_steps = 0
+        a.sweep_batches = []
     return a
 
 
@@ -375,6 +379,10 @@ def main():
     if rank == 0 and world == 1 and not args.no_shards:
         shards = shard_lines(tl, dl, args, ops, _lib, PhiloxNoise, EngineStep)
 
+    sweep = None
+    if rank == 0 and world == 1 and args.sweep_batches:
+        sweep = sweep_lines(args, ops, _lib, PhiloxNoise, EngineStep, dev)
+
     stream = None
     if args.stream_steps > 0:   # every rank: batch-level data parallelism (bit-exact), weak scaling
         stream = stream_line(tl, dl, row0, args, ops, _lib, StreamNoise, dp, dev, dist, world, rank)
@@ -445,6 +453,7 @@ def main():
             "kernels": kernels,
             "phases_ms": {"draws": ms_per_step - verify_ms, "verify": verify_ms},
             "stream": stream,
+            "sweep": sweep,
             "strong_scaling": strong,
             "shard_rows": shards,
             "configs1": cfg1,
@@ -523,6 +532,45 @@ def shard_lines(tl, dl, args, ops, _lib, PhiloxNoise, EngineStep):
         res[f"rows{rows}"] = {"rows_per_gpu": rows, "n_gpus_for_global_32": n_gpus,
                               "ms_per_step": dt / steps * 1e3, "tokens_per_s_per_gpu": tokens / dt,
                               "projected_global_tokens_per_s": n_gpus * tokens / dt}
+    return res
+
+
+def sweep_lines(args, ops, _lib, PhiloxNoise, EngineStep, dev):
+    """SURVEY §8(d)'s large-batch roofline: the same engine step (configs[2]'s γ, V, logit
+    distributions, Philox noise) at B = --sweep-batches rows on this GPU, hipGraph replays, with the
+    verify path the library reports.  step_bytes = every target and drafter row once (2·γ·B·V·2);
+    traffic_bytes adds the one re-read the residual resample cannot avoid: the decided target and
+    drafter row of each sequence (2·B·V·2), so frac_traffic is the fraction of HBM peak the step's
+    necessary reads run at."""
+    res = {}
+    g, V = args.gamma, args.vocab
+    for B in args.sweep_batches:
+        tl, dl = engine_logits(B, g, V, args.sigma, 5000 + B, dev)
+        noise = PhiloxNoise(seed=4646 + B, offset_dev=torch.zeros(1, dtype=torch.long, device=dev))
+        st = EngineStep(tl, dl, noise, 0, ops, _lib)
+        for _ in range(3):
+            st()
+        torch.cuda.synchronize()
+        path = _lib.last_verify_path()
+        steps = 40
+        graph, _, replays = graph_steps(st, steps, 10, noise, g + 1, min_replays=4)
+        st.read_counts()
+        dts = [timed_replays(graph, replays, None) for _ in range(3)]
+        c = st.read_counts()
+        dt = statistics.median(dts)
+        vgraph, _, vrep = graph_steps(st.verify, steps, 10)
+        vdt = statistics.median(timed_replays(vgraph, vrep, None) for _ in range(3))
+        step_bytes = 2 * g * B * V * 2
+        traffic = step_bytes + 2 * B * V * 2
+        ms = dt / steps * 1e3
+        res[f"b{B}"] = {"rows": B, "verify_path": _lib.PATH_NAMES.get(path, str(path)), "ms_per_step": ms,
+                        "ms_per_step_trials": [d / steps * 1e3 for d in dts],
+                        "verify_ms": vdt / steps * 1e3, "draw_ms": (ms - vdt / steps * 1e3) / g,
+                        "tokens_per_s": float(c[:, 1].sum()) / (3 * dt),
+                        "step_bytes": step_bytes, "frac": step_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "traffic_bytes": traffic, "frac_traffic": traffic / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        del graph, vgraph, st, tl, dl
+        torch.cuda.empty_cache()
     return res
 
 

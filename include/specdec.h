@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define SD_ABI_VERSION 10
+#define SD_ABI_VERSION 11
 #define SD_MAX_GAMMA 32          /* drafts per call; specdec_amd.ops chunks longer windows */
 #define SD_NGRAM_MAX_FILLER 64   /* sd_ngram_verify filler_k                                    */
 
@@ -266,8 +266,11 @@ const char* sd_status_string(int32_t status);
  * with other work (another process, RCCL kernels, a side stream) may not be: the bounded polls
  * then flag rows SD_ROW_EXCHANGE_TIMEOUT.  allow_poll = 0 selects the arrival-counter exchanges
  * everywhere (no kernel waits on another workgroup); 1 (default) lets the occupancy check decide.
- * spin_limit bounds every poll (re-reads with s_sleep between them; 0 = the default 65536, < 0 =
- * give up at once — a test hook that forces the timeout path).  Process-wide; the environment
+ * spin_limit bounds every poll in MICROSECONDS OF WALL CLOCK (ABI 11; the device's constant
+ * 100 MHz s_memrealtime): 0 = the default 2,000,000 (2 s), < 0 = give up at once — a test hook
+ * that forces the timeout path.  A grid that shares the GPU with a long kernel of another stream
+ * therefore waits for that kernel (its producers are dispatched in order behind it) instead of
+ * flagging rows; only a record that never comes costs the bound.  Process-wide; the environment
  * variables SD_POLL (0/1) and SD_POLL_SPIN_LIMIT set the initial values.                       */
 int32_t sd_set_poll_policy(int32_t allow_poll, int32_t spin_limit);
 int32_t sd_get_poll_policy(int32_t* allow_poll, int32_t* spin_limit);

@@ -257,9 +257,19 @@ __device__ __forceinline__ void flag_error(int32_t* acc, int32_t status) {
     if (acc && e) __hip_atomic_fetch_or(acc, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Bounded polls: `limit` re-reads at most (the host's spin limit, sd_set_poll_policy); a negative
+// Bounded polls, by WALL CLOCK: a wait gives up after `limit_us` microseconds (the host's poll
+// bound, sd_set_poll_policy; default 2 s) of s_memrealtime (a constant 100 MHz clock), so a grid
+// that shares the GPU with a long kernel of another stream waits for it instead of flagging its
+// rows.  The clock is read once every 64 re-reads (the start of the wait at the 64th: the common
+// short waits never read it); t0 is the caller's per-wait state, zero before the loop.  A negative
 // limit gives up at once (tests force the timeout path with it).
-__device__ __forceinline__ bool spin_more(int spin, int limit) { return spin < limit; }
+__device__ __forceinline__ bool spin_more(int spin, int limit_us, uint64_t& t0) {
+    if (limit_us < 0) return false;
+    if ((spin & 63) != 63) return true;
+    const uint64_t t = __builtin_amdgcn_s_memrealtime();
+    if (spin == 63) t0 = t;
+    return t - t0 < (uint64_t)limit_us * 100u;
+}
 
 // ---------------------------------------------------------------- exp
 // e^x with v_exp_f32 (2^t) and the rounding error of t = x*log2(e) folded back in by FMA:

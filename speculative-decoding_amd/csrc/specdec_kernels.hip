@@ -1046,7 +1046,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                     const double t_n = lthr[bn * g + (in ? lane : 0)];
                     const uint64_t stp_n = lstpm[bn];
                     const bool ract_n = lact[bn * g] != 0;
-                    if (lane == (bi & 63)) { my_a = a; my_k = k; }
+                    if (bi < kWave && lane == bi) { my_a = a; my_k = k; }
                     if (bi >= kWave && lane == 0) { la[bi] = a; lk[bi] = k; }
                     const bool acc = spec ? !((double)u > t) : (double)u < t;
                     const uint64_t rej = __ballot(in && !acc);
@@ -1263,7 +1263,7 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
                 if (need[k]) {
                     const uint32_t tag = stats_tag(ep, b, s, lane);
                     uint4 rr = r[k];
-                    for (int spin = 0; rr.z != tag && spin_more(spin, P.spin_limit); ++spin) {
+                    uint64_t sw_ = 0; for (int spin = 0; rr.z != tag && spin_more(spin, P.spin_limit, sw_); ++spin) {
                         __builtin_amdgcn_s_sleep(1);
                         rr = ld_coh16(rp[k]);
                     }
@@ -2062,8 +2062,8 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
                 uint4 v = ld_coh16(rp + k);
                 if (poll_epoch) {   // poll mode: re-read until the record carries this call's tag (bounded)
                     const uint32_t tag = sample_tag(*poll_epoch, b, k);
-                    for (int spin = 0; v.w != tag; ++spin) {
-                        if (!spin_more(spin, P.spin_limit)) { atomicOr(&s_xstat, SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST); break; }
+                    uint64_t sw_ = 0; for (int spin = 0; v.w != tag; ++spin) {
+                        if (!spin_more(spin, P.spin_limit, sw_)) { atomicOr(&s_xstat, SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST); break; }
                         __builtin_amdgcn_s_sleep(1);
                         v = ld_coh16(rp + k);
                     }
@@ -2095,7 +2095,7 @@ __device__ __forceinline__ void sample_finish(const Plan& P, const Decision& d, 
                     const uint4* cr = P.crec + (int64_t)b * P.rn_chunks + c;
                     const uint32_t tag = sample_tag(*poll_epoch, b, c) ^ 0x5bd1e995u;
                     uint4 v = ld_coh16(cr);
-                    for (int spin = 0; v.w != tag && spin_more(spin, P.spin_limit); ++spin) {
+                    uint64_t sw_ = 0; for (int spin = 0; v.w != tag && spin_more(spin, P.spin_limit, sw_); ++spin) {
                         __builtin_amdgcn_s_sleep(1);
                         v = ld_coh16(cr);
                     }
@@ -2350,13 +2350,13 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
         bool have = lane >= 2;
         uint4 r = make_uint4(0u, 0u, 0u, 0u);
         const uint32_t tag = lane < 2 ? dec_tag(ep, b, lane) : 0u;
-        for (int spin = 0;; ++spin) {
+        uint64_t sw_ = 0; for (int spin = 0;; ++spin) {
             if (!have && P.spin_limit >= 0) {   // < 0: the test hook, the decision counts as lost
                 r = ld_coh16(P.drec + 2 * b + lane);
                 have = r.w == tag;
             }
             if (__all(have)) break;
-            if (!spin_more(spin, P.spin_limit)) break;   // bounded: the finisher flags the row
+            if (!spin_more(spin, P.spin_limit, sw_)) break;   // bounded: the finisher flags the row
             __builtin_amdgcn_s_sleep(SD_SAMP_SLEEP);   // the decision is microseconds away
         }
         if (lane < 2) s_rec[lane] = r;
@@ -2478,7 +2478,7 @@ __device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decisio
         const float4* rp = reinterpret_cast<const float4*>(P.sprec) + (int64_t)b * P.rn_chunks;
         for (int k = threadIdx.x; k < P.rn_chunks; k += kThreads) {
             const uint32_t tag = sample_tag(epoch, b, k);
-            for (int spin = 0; ld_coh16(rp + k).w != tag && spin_more(spin, P.spin_limit); ++spin)
+            uint64_t sw_ = 0; for (int spin = 0; ld_coh16(rp + k).w != tag && spin_more(spin, P.spin_limit, sw_); ++spin)
                 __builtin_amdgcn_s_sleep(1);
         }
     }
@@ -3138,7 +3138,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             have[q] = !(q < npass && k < A.n_span) || k == c;
             rec[q] = make_uint4(0u, 0u, 0u, 0u);
         }
-        for (int spin = 0;; ++spin) {
+        uint64_t sw_ = 0; for (int spin = 0;; ++spin) {
             if (A.spin_limit >= 0) {   // < 0: the test hook, every record counts as lost
 #pragma unroll
                 for (int q = 0; q < 2; ++q) {
@@ -3149,7 +3149,7 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
                 }
                 if (__all(have[0] && have[1])) break;
             }
-            if (!spin_more(spin, A.spin_limit)) {   // bounded: ~tens of ms; the row is flagged, never a hang
+            if (!spin_more(spin, A.spin_limit, sw_)) {   // bounded: ~tens of ms; the row is flagged, never a hang
                 xstat = SD_ROW_EXCHANGE_TIMEOUT | SD_ROW_INVALID_DIST;
                 break;
             }
@@ -3328,7 +3328,7 @@ thread_local hipError_t g_last_error = hipSuccess;
 
 // In-launch exchange policy (sd_set_poll_policy): whether poll-mode exchanges may be chosen at all,
 // and the bound of every poll.  Process-wide; SD_POLL / SD_POLL_SPIN_LIMIT set the initial values.
-constexpr int kDefaultSpin = 1 << 16;
+constexpr int kDefaultSpin = 2000000;   // us of wall clock per wait (2 s): outlasts a co-running kernel
 std::atomic<int> g_allow_poll{-1};
 std::atomic<int> g_spin_limit{kDefaultSpin};
 std::once_flag g_policy_once;
@@ -3371,6 +3371,7 @@ int spin_limit() {
     policy_init();
     return g_spin_limit.load(std::memory_order_relaxed);
 }
+int resident_cap(const void* kern, int threads = sd::kThreads, size_t dyn = 0);
 }  // namespace
 
 #include "sd_threshold.inc"
@@ -3489,20 +3490,21 @@ int32_t launch_stats_dt(const sd::Plan& P, bool fast, int slot_lo, int slot_cnt,
     return SD_OK;
 }
 
-// resident capacity of a kernel's 256-thread workgroups on this device (occupancy x CUs), cached
-int resident_cap(const void* kern) {
+// resident capacity of a kernel's workgroups (256 threads unless given) on this device (occupancy x
+// CUs), cached per (device, kernel, block, dynamic LDS) under a mutex: any host thread may call
+int resident_cap(const void* kern, int threads, size_t dyn) {
     static std::mutex mu;
-    static std::map<std::pair<int, const void*>, int> caps;
+    static std::map<std::tuple<int, const void*, int, size_t>, int> caps;
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return 0;
     std::lock_guard<std::mutex> lk(mu);
-    auto it = caps.find({dev, kern});
+    auto it = caps.find({dev, kern, threads, dyn});
     if (it == caps.end()) {
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess ||
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, threads, dyn) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
             per_cu = cus = 0;
-        it = caps.emplace(std::make_pair(dev, kern), per_cu * cus).first;
+        it = caps.emplace(std::make_tuple(dev, kern, threads, dyn), per_cu * cus).first;
     }
     return it->second;
 }
@@ -3653,17 +3655,8 @@ int32_t launch_draw_lean_t(const sd::Plan& P, void* stream) {
     A.pstride = (A.n_span + 7) & ~7;
     // poll mode needs every row's consumer resident while it waits: at most half the workgroups
     // the device holds at once (occupancy x CUs, queried once per device) are consumers
-    static int cap[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
-    if (cap[dev] == 0) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_draw_lean<DT, NST, GREEDY>, kThreads, 0) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            per_cu = cus = 0;
-        cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
-    }
-    A.poll = cap[dev] > 0 && 2 * P.B <= cap[dev] && poll_allowed();
+    const int cap = resident_cap((const void*)k_draw_lean<DT, NST, GREEDY>);
+    A.poll = cap > 0 && 2 * P.B <= cap && poll_allowed();
     A.spin_limit = P.spin_limit;
     A.status_or = P.status_or;
     A.ts = P.ts;
@@ -3761,19 +3754,9 @@ int32_t launch_draw_stream(const sd::Plan& P, void* stream) {
     const int n_span = (int)((P.V + kThreads * 8 - 1) / (kThreads * 8));
     if (!al || P.V < 8 || n_span > 128) return 0;
     if ((int64_t)n_span * sd::kDsRecs * 16 > (int64_t)(max_chunks(P.V) + 1) * (int64_t)sizeof(sd::ResPart)) return 0;
-    static int cap[2][64];
-    const int di = P.tdt == SD_BF16 ? 0 : 1;
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (cap[di][dev] == 0) {
-        int per_cu = 0, cus = 0;
-        const void* kern = P.tdt == SD_BF16 ? (const void*)sd::k_draw_stream<SD_BF16> : (const void*)sd::k_draw_stream<SD_F16>;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kThreads, 0) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            per_cu = cus = 0;
-        cap[di][dev] = per_cu * cus > 0 ? per_cu * cus : -1;
-    }
-    if (cap[di][dev] <= 0 || 2 * P.B > cap[di][dev]) return 0;
+    const int cap = resident_cap(P.tdt == SD_BF16 ? (const void*)sd::k_draw_stream<SD_BF16>
+                                                  : (const void*)sd::k_draw_stream<SD_F16>);
+    if (cap <= 0 || 2 * P.B > cap) return 0;
     sd::DrawStream A{};
     A.rows = static_cast<const char*>(P.trow[0]);
     A.stride_bytes = P.tstride * 2;
@@ -3816,9 +3799,10 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
         // one 2048-element span per workgroup (4096-element spans measured slower)
         const int64_t span = (int64_t)kThreads * 8;
         if (fast && al && P.V >= 8 && (P.V + span - 1) / span <= 128) {
-            g_sample_path = SD_PATH_SAMPLE_DRAW_LEAN;
-            if (P.tdt == SD_BF16) return launch_draw_lean_t<SD_BF16, 1>(P, stream);
-            return launch_draw_lean_t<SD_F16, 1>(P, stream);
+            const int32_t st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 1>(P, stream)
+                                                : launch_draw_lean_t<SD_F16, 1>(P, stream);
+            if (st == SD_OK) g_sample_path = SD_PATH_SAMPLE_DRAW_LEAN;   // only once the launch succeeded
+            return st;
         }
     }
     // spans of NST stages (2048 elements each): 2 once the grid passes ~1024 workgroups
@@ -3832,10 +3816,11 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
     P.n_chunks = (int32_t)((P.V + P.chunk - 1) / P.chunk);
     P.rn_chunks = P.n_chunks;   // pick_chunk's count
     P.xcd_affine = P.B % 8 == 0;
-    g_sample_path = SD_PATH_SAMPLE_DRAW;
-    if (P.tdt == SD_BF16) return launch_draw_dt<SD_BF16>(P, nst, stream);
-    if (P.tdt == SD_F32) return launch_draw_dt<SD_F32>(P, nst, stream);
-    return launch_draw_dt<SD_F16>(P, nst, stream);
+    const int32_t st = P.tdt == SD_BF16 ? launch_draw_dt<SD_BF16>(P, nst, stream)
+                     : P.tdt == SD_F32  ? launch_draw_dt<SD_F32>(P, nst, stream)
+                                        : launch_draw_dt<SD_F16>(P, nst, stream);
+    if (st == SD_OK) g_sample_path = SD_PATH_SAMPLE_DRAW;
+    return st;
 }
 
 // The nucleus drafter draw by rejection (k_draw_nuc, sd_draw_nucleus.inc) in place of the threshold
@@ -3852,17 +3837,8 @@ int32_t launch_draw_nuc(const sd::Plan& P, const sd_processor& proc, void* strea
     if (nsl > kWave || P.B > kCntMax || sd::kThrSlice != 4 * sd::kSubSlice) return 0;
     // the records (kNucRecs x 16 B per slice) inside the row's share of the ResPart region
     if ((int64_t)nsl * sd::kNucRecs * 16 > (int64_t)(max_chunks(P.V) + 1) * (int64_t)sizeof(sd::ResPart)) return 0;
-    static int cap[64];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    if (cap[dev] == 0) {
-        int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, sd::k_draw_nuc<SD_BF16>, sd::kNucThreads, 0) != hipSuccess ||
-            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            per_cu = cus = 0;
-        cap[dev] = per_cu * cus > 0 ? per_cu * cus : -1;
-    }
-    if (cap[dev] <= 0 || (int64_t)nsl * P.B > cap[dev]) return 0;
+    const int cap = resident_cap((const void*)sd::k_draw_nuc<SD_BF16>, sd::kNucThreads);
+    if (cap <= 0 || (int64_t)nsl * P.B > cap) return 0;
     sd::NucArgs A{};
     A.rows = static_cast<const char*>(P.trow[0]);
     A.stride_bytes = P.tstride * 2;

@@ -9,7 +9,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-SD_ABI_VERSION = 10
+SD_ABI_VERSION = 11
 SD_MAX_GAMMA = 32           # drafts per call (ops.verify / ngram_verify chunk longer windows)
 SD_NGRAM_MAX_FILLER = 64
 
@@ -258,8 +258,9 @@ def check(status: int, what: str):
 
 def set_poll_policy(allow_poll: bool = True, spin_limit: int = 0) -> None:
     """sd_set_poll_policy: whether kernels may exchange partials by polling inside one launch (the
-    occupancy check still decides per launch), and the bound of every poll (0 = default; < 0 gives
-    up at once — a test hook that forces the SD_ROW_EXCHANGE_TIMEOUT path)."""
+    occupancy check still decides per launch), and the bound of every poll in microseconds of wall
+    clock (0 = the default 2 s; < 0 gives up at once — a test hook that forces the
+    SD_ROW_EXCHANGE_TIMEOUT path)."""
     check(lib.sd_set_poll_policy(1 if allow_poll else 0, int(spin_limit)), "sd_set_poll_policy")
 
 

@@ -11,7 +11,9 @@ engine state, words of the torch generator consumed — is the one call over the
   exactly where its chunk k stopped: it runs only for rows that accepted every draft of chunk k
   without finishing (``active``), with the engine state's ``step`` advanced by the chunk start.
   Under STREAM noise the calls go row by row (each row's chunks in order, the generator moved by
-  each call's device count), so the words are consumed in the reference's row-serial order; under
+  each call's device count), so the words are consumed in the reference's row-serial order — B·⌈γ/32⌉
+  calls, each ending in a device→host read of the words used: exact, but slow at engine batch sizes
+  (a chunked STREAM window is a parity tool; Philox windows of any length are one call per chunk); under
   Philox every chunk runs on all rows at once.  Afterwards the window's tail past each stopped row's
   last accepted draft is zeroed, as :332-336 does for the whole window.
 * SPEC (rule A8, :139-171).  ``r = rand(γ)`` is drawn for the whole window before anything else,

@@ -283,6 +283,10 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
     tokens emitted) to every row's pair (the A12 bookkeeping, kept on the device).
     """
     gamma = len(draft_rows)
+    if rule == _lib.SD_RULE_SPEC and (active is not None or engine_state is not None):
+        # the batch-1 rule has no finished rows and no engine state (sampling/speculative_decoding.py:
+        # 129-171); refused on every path, so a γ > SD_MAX_GAMMA window cannot drop them silently
+        raise ValueError("active / engine_state belong to the ENGINE rule (SD_RULE_ENGINE)")
     if gamma > _lib.SD_MAX_GAMMA:   # the reference takes any γ: windows of <= SD_MAX_GAMMA drafts (chunked.py)
         if prof_events is not None:
             raise ValueError("prof_events needs gamma <= SD_MAX_GAMMA")

@@ -104,6 +104,9 @@ SPEC_GRID = [
     (4, 4, 128256, torch.bfloat16, "nucleus05_t07", 22),
     (4, 4, 128256, torch.bfloat16, "topknucleus", 23),
     (4, 8, 128256, torch.bfloat16, "nucleus09", 24),
+    # more than one wave of rows in one STREAM k_walk block
+    (96, 1, 2048, torch.bfloat16, "multi_t1", 25),
+    (80, 2, 2048, torch.bfloat16, "multi_t07", 26),
 ]
 
 
@@ -304,6 +307,10 @@ ENGINE_GRID = [
     (5, 3, 2048, torch.bfloat16, 3),
     (32, 4, 128256, torch.bfloat16, 4),
     (8, 4, 50257, torch.float32, 5),
+    # more than one wave of rows in one k_walk block (STREAM): rows >= 64 walk off lane registers
+    (96, 1, 2048, torch.bfloat16, 9),
+    (80, 2, 2048, torch.bfloat16, 10),
+    (128, 4, 4096, torch.bfloat16, 11),
 ]
 
 
