@@ -276,7 +276,7 @@ int32_t sd_set_poll_policy(int32_t allow_poll, int32_t spin_limit);
 int32_t sd_get_poll_policy(int32_t* allow_poll, int32_t* spin_limit);
 const char* sd_last_hip_error(void);   /* hipGetErrorString of the last failed launch (this thread) */
 
-/* Dispatch options (ABI 10): switches between kernel paths that compute the same outputs, for
+/* Dispatch options (ABI 10, 11): switches between kernel paths that compute the same outputs, for
  * A/B runs and for tests that compare the paths.  Process-wide, set by the caller; no entry point
  * reads the environment (SD_POLL / SD_POLL_SPIN_LIMIT seed the poll policy once, at first use).
  * sd_set_option returns SD_ERR_INVALID for an unknown option or value.                        */
@@ -288,6 +288,13 @@ typedef enum {
                                    grid is resident; 0: the launch-per-phase design               */
     SD_OPT_DRAW_STREAM = 4,     /* 1 (default): STREAM multinomial draws in one pass
                                    (k_draw_stream); 0: statistics + race + finalize launches      */
+    SD_OPT_FUSED_TICKET = 5,    /* ABI 11. -1 (default): k_verify_fused in ticket order (work items
+                                   by arrival ticket: any batch, resident or not) for B >= 64 or a
+                                   grid too big to be resident; 0: block-id order only (a grid
+                                   that is not resident takes k_stats + k_sample); 1: always      */
+    SD_OPT_DRAW_SPAN = 6,       /* ABI 11. 0 (default): k_draw_lean's span per workgroup chosen by
+                                   the batch (2048 elements, more for large batches); 1 / 2 / 4:
+                                   that many 2048-element stages per workgroup                    */
 } sd_option;
 int32_t sd_set_option(int32_t option, int32_t value);
 int32_t sd_get_option(int32_t option, int32_t* value);
@@ -300,6 +307,7 @@ typedef enum {
     SD_PATH_VERIFY_FUSED = 2,       /* k_verify_fused: one launch                                 */
     SD_PATH_VERIFY_TWO_LAUNCH = 3,  /* k_stats (+ decider) then k_sample                          */
     SD_PATH_VERIFY_STREAM = 4,      /* STREAM: k_stats, k_decide, k_walk, k_resample, k_finalize  */
+    SD_PATH_VERIFY_FUSED_TICKET = 5,/* k_verify_fused in ticket order (ABI 11): one launch, any B  */
     SD_PATH_SAMPLE_DRAW_LEAN = 16,  /* k_draw_lean (PHILOX multinomial, T = 1, 16-bit)           */
     SD_PATH_SAMPLE_DRAW = 17,       /* k_draw (PHILOX, processors / fp32)                          */
     SD_PATH_SAMPLE_NUCLEUS = 18,    /* k_draw_nuc (PHILOX nucleus by rejection)                    */

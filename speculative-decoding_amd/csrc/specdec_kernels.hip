@@ -115,6 +115,9 @@ struct Plan {
     uint4* drec;          // fused verify: per sequence two tagged decision records for its samplers
     uint4* crec;          // fused verify, split records: the chunks' candidates, apart from their totals
     int32_t n_samp;       // fused verify (k_stats<.., SAMP>): sampling workgroups per sequence
+    int32_t ticket;       // fused verify, any batch: work items by arrival ticket (fused_role), not block id
+    int32_t lag;          //   ticket mode: sequence b's samplers come after sequence b + lag's spans
+    uint32_t* ticket_ctr; //   ticket mode: the launch's ticket counter (zero between launches)
     int32_t* keep_hist;   // threshold scratch
     uint32_t* thr_part;   // 16-bit thresholds (sd_threshold.inc): per (row, slice) max key | NaN-inf flag
     float* thr_tail;      //   per (row, slice) Σexp below the window / tie counts
@@ -416,6 +419,31 @@ __device__ __forceinline__ void affine_split(int id, int per_seq, int& b, int& i
     item = k % per_seq;
 }
 
+// Ticket mode's schedule (stats_body): units u = 0 .. B + lag - 1; unit u holds sequence u's
+// per_seq items (its spans, then its decider) when u < B, then sequence (u - lag)'s n_samp
+// samplers when u >= lag.  Ticket t -> (sequence b, item) or (sequence b, sampler samp).
+__device__ __forceinline__ void fused_role(const Plan& P, int t, int per_seq, int& b, int& item, int& samp) {
+    const int D = P.lag, ns = P.n_samp, full = per_seq + ns;
+    samp = -1;
+    item = 0;
+    if (t < D * per_seq) {                       // units 0 .. lag-1: spans and deciders only
+        b = t / per_seq;
+        item = t - b * per_seq;
+        return;
+    }
+    t -= D * per_seq;
+    if (t < (P.B - D) * full) {                  // units lag .. B-1: both
+        const int u = t / full, k = t - u * full;
+        if (k < per_seq) { b = D + u; item = k; }
+        else { b = u; samp = k - per_seq; }
+        return;
+    }
+    t -= (P.B - D) * full;                       // units B .. B+lag-1: samplers only
+    const int u = t / ns;
+    b = P.B - D + u;
+    samp = t - u * ns;
+}
+
 template <int DT, bool FAST>
 __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int wg_id);
 template <int DT, bool FAST>
@@ -451,7 +479,31 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     int b, s, chunk;
     bool decider = false;
     int samp = -1;
-    if (SAMP && wg_id >= P.B * per_seq) {
+    if (SAMP && P.ticket) {
+        // Ticket mode (any batch; the grid need not be resident): a workgroup's work item is the
+        // arrival ticket it takes, not its block id.  Every wait points at an EARLIER ticket — a
+        // decider at its spans, a sampler at its decider — whose holder is already running, so the
+        // launch always progresses whatever else holds the CUs; the one wait on later tickets (a
+        // decider for its samplers, `lag` sequences on) holds at most lag + 1 workgroups.  The items
+        // run sequence by sequence — spans, decider — with sequence b's samplers after sequence
+        // b + lag's items (fused_role): by then b's decision is about out, so samplers do not sit in
+        // slots the spans stream with, and they re-read the decided target row while the Infinity
+        // Cache still holds it.
+        __shared__ uint32_t s_tk;
+        if (threadIdx.x == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(P.ticket_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the launch's last ticket: every other has been taken, re-arm the counter
+            if (t + 1u == (uint32_t)P.B * (uint32_t)(per_seq + P.n_samp))
+                __hip_atomic_store(P.ticket_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_tk = t;
+        }
+        __syncthreads();
+        int item;
+        fused_role(P, (int)s_tk, per_seq, b, item, samp);
+        decider = samp < 0 && item == n_span;
+        s = slot_lo + (samp < 0 && item < n_span ? item / gx : 0);
+        chunk = samp < 0 && item < n_span ? item % gx : 0;
+    } else if (SAMP && wg_id >= P.B * per_seq) {
         // the samplers come after every span and decider in dispatch order (block id): they only wait
         // for a decision, so the spans, which wait for nothing, always get their slots first, and a
         // sampler frees its slot once it has published.  Sequence b = id % B: with B % 8 == 0 every
@@ -3348,10 +3400,14 @@ void policy_init() {
 }
 
 // Dispatch options (sd_set_option), indexed by sd_option; relaxed reads on every call.
-std::atomic<int> g_opt_fused{1}, g_opt_lean{-1}, g_opt_thr_poll{1}, g_opt_draw_stream{1};
+std::atomic<int> g_opt_fused{1}, g_opt_lean{-1}, g_opt_thr_poll{1}, g_opt_draw_stream{1}, g_opt_ticket{-1};
+std::atomic<int> g_opt_draw_span{0};
+constexpr int kDrawSpan2MinB = 64, kDrawSpan4MinB = 256;   // k_draw_lean: batches above take 2 / 4 stages
 std::atomic<int>* option_slot(int32_t opt) {
     switch (opt) {
+        case SD_OPT_DRAW_SPAN: return &g_opt_draw_span;
         case SD_OPT_FUSED_VERIFY: return &g_opt_fused;
+        case SD_OPT_FUSED_TICKET: return &g_opt_ticket;
         case SD_OPT_LEAN_VERIFY: return &g_opt_lean;
         case SD_OPT_THRESHOLD_POLL: return &g_opt_thr_poll;
         case SD_OPT_DRAW_STREAM: return &g_opt_draw_stream;
@@ -3514,11 +3570,8 @@ int resident_cap(const void* kern, int threads, size_t dyn) {
 // samplers poll).  1 launched, 0 not applicable (the caller runs k_stats + k_sample), < 0 an error.
 template <int DT>
 int32_t launch_fused_dt(const sd::Plan& P, bool fast, void* stream) {
-    const void* kern = fast ? (const void*)k_verify_fused<DT, true> : (const void*)k_verify_fused<DT, false>;
     const int64_t head = (int64_t)P.B * (P.n_tslots * P.n_chunks + 1), total = head + (int64_t)P.B * P.n_samp;
-    // the spans and deciders resident at once with headroom (the deciders poll the spans); the
-    // samplers (after them in dispatch order) wait only for decisions and take freed slots
-    if (!poll_allowed() || 2 * head > resident_cap(kern)) return 0;
+    if (!poll_allowed()) return 0;
     sd::Plan Q = P;
     Q.kpoll = 1;
     if (fast) SD_LAUNCH((k_verify_fused<DT, true>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
@@ -3526,11 +3579,45 @@ int32_t launch_fused_dt(const sd::Plan& P, bool fast, void* stream) {
     return 1;
 }
 
+const void* fused_kernel(const sd::Plan& P) {
+    const bool fast = P.tT == 1.0f && P.dT == 1.0f && !P.t_keep && !P.d_keep;
+    if (P.tdt == SD_BF16) return fast ? (const void*)k_verify_fused<SD_BF16, true> : (const void*)k_verify_fused<SD_BF16, false>;
+    if (P.tdt == SD_F16) return fast ? (const void*)k_verify_fused<SD_F16, true> : (const void*)k_verify_fused<SD_F16, false>;
+    return fast ? (const void*)k_verify_fused<SD_F32, true> : (const void*)k_verify_fused<SD_F32, false>;
+}
+
 int32_t launch_fused(const sd::Plan& P, void* stream) {
     const bool fast = P.tT == 1.0f && P.dT == 1.0f && !P.t_keep && !P.d_keep;
     if (P.tdt == SD_BF16) return launch_fused_dt<SD_BF16>(P, fast, stream);
     if (P.tdt == SD_F16) return launch_fused_dt<SD_F16>(P, fast, stream);
     return launch_fused_dt<SD_F32>(P, fast, stream);
+}
+
+// The fused verify's work layout for F (n_samp set): block-id order when the spans and deciders are
+// resident at once with headroom (the deciders poll the spans; the samplers, after them in dispatch
+// order, wait only for decisions and take freed slots) and the batch is small; otherwise ticket
+// order (stats_body, fused_role) with spans of kTicketSpan elements — at any batch, resident or not.
+// SD_OPT_FUSED_TICKET: -1 auto, 0 never (a non-resident grid then takes the two launches), 1 always.
+// false: no fused launch for this batch.
+constexpr int kTicketMinB = 64;
+constexpr int kTicketSpan = 16 * kThreads * 8;   // 32768 elements: 4 spans per Llama-3 row
+bool fused_layout(sd::Plan& F) {
+    const int cap = resident_cap(fused_kernel(F));
+    const int64_t head = (int64_t)F.B * (F.n_tslots * F.n_chunks + 1);
+    const bool resident = cap > 0 && 2 * head <= cap;
+    const int tmode = opt(g_opt_ticket);
+    F.ticket = tmode == 1 || (tmode < 0 && (F.B >= kTicketMinB || !resident));
+    if (!F.ticket) return resident;
+    if (cap <= 0) return false;
+    F.chunk = kTicketSpan;
+    F.n_chunks = (F.V + F.chunk - 1) / F.chunk;
+    if (F.n_chunks > kWave) return false;
+    const int per_unit = F.n_tslots * F.n_chunks + 1 + F.n_samp;
+    F.lag = cap / per_unit;
+    F.lag = F.lag < 1 ? 1 : (F.lag > F.B ? F.B : F.lag);
+    F.ticket_ctr = F.cnt + ((size_t)1 * kCntMax + (kCntMax - 1)) * kCntStride;   // set 1's last counter
+    F.xcd_affine = 0;
+    return true;
 }
 
 int32_t launch_stats_group(const sd::Plan& P, int dt, bool fast, int slot_lo, int slot_cnt, bool tail, void* stream) {
@@ -3799,8 +3886,15 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
         // one 2048-element span per workgroup (4096-element spans measured slower)
         const int64_t span = (int64_t)kThreads * 8;
         if (fast && al && P.V >= 8 && (P.V + span - 1) / span <= 128) {
-            const int32_t st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 1>(P, stream)
-                                                : launch_draw_lean_t<SD_F16, 1>(P, stream);
+            // stages per workgroup: one 2048-element span while the grid is a few thousand
+            // workgroups; a large batch takes 2 or 4 stages per workgroup, so each holds more bytes
+            // in flight and the grid stays a few resident rounds (SD_OPT_DRAW_SPAN pins it)
+            int nst = opt(g_opt_draw_span);
+            if (nst == 0) nst = P.B <= kDrawSpan2MinB ? 1 : (P.B <= kDrawSpan4MinB ? 2 : 4);
+            int32_t st;
+            if (nst == 4) st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 4>(P, stream) : launch_draw_lean_t<SD_F16, 4>(P, stream);
+            else if (nst == 2) st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 2>(P, stream) : launch_draw_lean_t<SD_F16, 2>(P, stream);
+            else st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 1>(P, stream) : launch_draw_lean_t<SD_F16, 1>(P, stream);
             if (st == SD_OK) g_sample_path = SD_PATH_SAMPLE_DRAW_LEAN;   // only once the launch succeeded
             return st;
         }
@@ -3892,7 +3986,8 @@ int32_t sd_set_option(int32_t option, int32_t value) {
     std::atomic<int>* o = option_slot(option);
     if (!o) return SD_ERR_INVALID;
     const bool ok = option == SD_OPT_FUSED_VERIFY ? (value >= 0 && value <= 2)
-                  : option == SD_OPT_LEAN_VERIFY ? (value >= -1 && value <= 1)
+                  : option == SD_OPT_LEAN_VERIFY || option == SD_OPT_FUSED_TICKET ? (value >= -1 && value <= 1)
+                  : option == SD_OPT_DRAW_SPAN ? (value == 0 || value == 1 || value == 2 || value == 4)
                                                  : (value == 0 || value == 1);
     if (!ok) return SD_ERR_INVALID;
     o->store(value, std::memory_order_relaxed);
@@ -4028,12 +4123,13 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
             F.rchunk = kThreads * kFusedEpt;
             F.rn_chunks = (P.V + F.rchunk - 1) / F.rchunk;
             F.n_samp = (F.rn_chunks + 1) / 2;   // two chunks per sampler (fused_sampler)
+            const bool layout_ok = fused_layout(F);   // block-id or ticket order; may re-cut the spans
             // records: the spans' (srec = rpart), the samplers' totals after them, the decisions, the candidates
-            const size_t n_srec = (size_t)P.B * P.stat_slots * P.n_chunks;
+            const size_t n_srec = (size_t)P.B * P.stat_slots * F.n_chunks;
             const size_t need = n_srec + 2 * (size_t)P.B * F.rn_chunks + 2 * (size_t)P.B + 8;
             const size_t have = (size_t)(P.B > a->batch * (2 * a->gamma + 1) ? P.B : a->batch * (2 * a->gamma + 1)) *
                                 (max_chunks(P.V) + 1) * sizeof(ResPart) / sizeof(uint4);
-            if (F.rn_chunks <= kTailChunks && need <= have) {
+            if (layout_ok && F.rn_chunks <= kTailChunks && need <= have) {
                 F.sprec = F.srec + n_srec;
                 F.drec = F.sprec + (size_t)P.B * F.rn_chunks;
                 // chunk candidates in records of their own (sample_chunk_pick): the totals go out
@@ -4041,7 +4137,7 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
                 F.crec = F.drec + 2 * (size_t)P.B;
                 const int32_t st = launch_fused(F, stream);
                 if (st < 0) return st;
-                if (st) { g_verify_path = SD_PATH_VERIFY_FUSED; return SD_OK; }
+                if (st) { g_verify_path = F.ticket ? SD_PATH_VERIFY_FUSED_TICKET : SD_PATH_VERIFY_FUSED; return SD_OK; }
             }
         }
     }

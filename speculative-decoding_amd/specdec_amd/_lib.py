@@ -34,11 +34,14 @@ SD_ROW_ERROR_MASK = SD_ROW_INVALID_DIST | SD_ROW_NOISE_OVERRUN | SD_ROW_EXCHANGE
 
 # dispatch options (sd_set_option) and the paths sd_last_*_path reports
 SD_OPT_FUSED_VERIFY, SD_OPT_LEAN_VERIFY, SD_OPT_THRESHOLD_POLL, SD_OPT_DRAW_STREAM = 1, 2, 3, 4
+SD_OPT_FUSED_TICKET, SD_OPT_DRAW_SPAN = 5, 6
 SD_PATH_NONE = 0
 SD_PATH_VERIFY_LEAN, SD_PATH_VERIFY_FUSED, SD_PATH_VERIFY_TWO_LAUNCH, SD_PATH_VERIFY_STREAM = 1, 2, 3, 4
+SD_PATH_VERIFY_FUSED_TICKET = 5
 SD_PATH_SAMPLE_DRAW_LEAN, SD_PATH_SAMPLE_DRAW, SD_PATH_SAMPLE_NUCLEUS, SD_PATH_SAMPLE_STREAM = 16, 17, 18, 19
 SD_PATH_SAMPLE_GREEDY_LEAN, SD_PATH_SAMPLE_MULTI = 20, 21
 PATH_NAMES = {SD_PATH_NONE: "none", SD_PATH_VERIFY_LEAN: "k_verify_lean", SD_PATH_VERIFY_FUSED: "k_verify_fused",
+              SD_PATH_VERIFY_FUSED_TICKET: "k_verify_fused(ticket)",
               SD_PATH_VERIFY_TWO_LAUNCH: "k_stats+k_sample", SD_PATH_VERIFY_STREAM: "stream",
               SD_PATH_SAMPLE_DRAW_LEAN: "k_draw_lean", SD_PATH_SAMPLE_DRAW: "k_draw", SD_PATH_SAMPLE_NUCLEUS: "k_draw_nuc",
               SD_PATH_SAMPLE_STREAM: "k_draw_stream", SD_PATH_SAMPLE_GREEDY_LEAN: "k_draw_lean<greedy>",

@@ -67,21 +67,30 @@ def run(tl, dl, rule, spec, seed, engine=False, verify_ctx=contextlib.nullcontex
 PROCS = [("multinomial", 1.0, 0, 0.0), ("multinomial", 0.7, 0, 0.0), ("topk", 1.0, 50, 0.0)]
 
 
-@pytest.mark.parametrize("B,V", [(8, 128256), (32, 128256), (16, 50257)])
+def ticket(value):
+    from specdec_amd import _lib
+    return _lib.option(_lib.SD_OPT_FUSED_TICKET, value)
+
+
+@pytest.mark.parametrize("B,V,tk", [(8, 128256, -1), (32, 128256, -1), (16, 50257, -1),
+                                    # ticket order: forced at small batches, by default from B = 64
+                                    (8, 128256, 1), (32, 128256, 1), (128, 128256, -1), (300, 50257, -1)])
 @pytest.mark.parametrize("rule", ["engine", "spec"])
 @pytest.mark.parametrize("proc", PROCS, ids=[f"{p[0]}-T{p[1]}" for p in PROCS])
-def test_fused_verify_equals_two_launch_verify(B, V, rule, proc):
+def test_fused_verify_equals_two_launch_verify(B, V, tk, rule, proc):
     from specdec_amd import ops
     spec = ops.ProcSpec(*proc)
     seed = 31 * B + V % 89 + (1 if rule == "spec" else 2)
     tl, dl = inputs(B, 4, V, rule, seed)
     engine = rule == "engine"
     from specdec_amd import _lib
-    with fused(1):
+    with fused(1), ticket(tk):
         a = run(tl, dl, rule, spec, seed, engine)
     with fused(0):
         b = run(tl, dl, rule, spec, seed, engine)
-    assert int(a.pop("path")) == _lib.SD_PATH_VERIFY_FUSED
+    want = _lib.SD_PATH_VERIFY_FUSED_TICKET if tk == 1 or B >= 64 else _lib.SD_PATH_VERIFY_FUSED
+    pa = int(a.pop("path"))
+    assert pa == want, _lib.PATH_NAMES.get(pa)
     assert int(b.pop("path")) == _lib.SD_PATH_VERIFY_TWO_LAUNCH
     for k in a:
         assert torch.equal(a[k].nan_to_num(), b[k].nan_to_num()), (k, a[k], b[k])

@@ -82,13 +82,17 @@ def verify(sd, tl, dl, ids, rule, proc, noise, stops=(), draft_is_probs=False, d
 
 
 def expect_path(sd, out, B, draws, stochastic=True):
-    """With the draws' stats, B >= 8 stochastic calls take k_verify_fused, B <= 8 k_verify_lean (where
-    both apply, the lean kernel first: B == 8 bf16 plain rows)."""
+    """With the draws' stats, B >= 8 stochastic calls take k_verify_fused (in ticket order from B = 64),
+    B <= 8 k_verify_lean (where both apply, the lean kernel first: B == 8 bf16 plain rows)."""
     if not draws or not stochastic:
         return
-    assert out.path in (sd.lib.SD_PATH_VERIFY_FUSED, sd.lib.SD_PATH_VERIFY_LEAN) if B == 8 else \
-        out.path == (sd.lib.SD_PATH_VERIFY_FUSED if B > 8 else sd.lib.SD_PATH_VERIFY_LEAN), \
-        sd.lib.PATH_NAMES.get(out.path)
+    if B == 8:
+        want = (sd.lib.SD_PATH_VERIFY_FUSED, sd.lib.SD_PATH_VERIFY_LEAN)
+    elif B >= 64:
+        want = (sd.lib.SD_PATH_VERIFY_FUSED_TICKET,)
+    else:
+        want = (sd.lib.SD_PATH_VERIFY_FUSED if B > 8 else sd.lib.SD_PATH_VERIFY_LEAN,)
+    assert out.path in want, sd.lib.PATH_NAMES.get(out.path)
 
 
 def chi2_check(samples, probs, label):
@@ -198,7 +202,9 @@ def test_perf_spec_accept_walk(sd, kind, V, B, dtype, draws):
 @pytest.mark.parametrize("draws", [False, True], ids=["stats-in-verify", "stats-from-draws"])
 @pytest.mark.parametrize("B,V,dtype", [(16, 4096, torch.bfloat16), (32, 128256, torch.bfloat16),
                                        (8, 50257, torch.float32), (8, 128256, torch.bfloat16),
-                                       (32, 50257, torch.bfloat16)])
+                                       (32, 50257, torch.bfloat16),
+                                       # the large-batch sweep's shapes (ticket-order fused verify)
+                                       (128, 128256, torch.bfloat16), (512, 32768, torch.bfloat16)])
 def test_perf_engine_accept_walk_and_state(sd, B, V, dtype, draws):
     g, step, gen_len = 4, 4, 12
     tl = rand_logits((B, g, V), dtype, 21)
