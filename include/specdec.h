@@ -37,7 +37,8 @@ extern "C" {
 
 #define SD_ABI_VERSION 11
 #define SD_MAX_GAMMA 32          /* drafts per call; specdec_amd.ops chunks longer windows */
-#define SD_NGRAM_MAX_FILLER 64   /* sd_ngram_verify filler_k                                    */
+#define SD_NGRAM_MAX_FILLER 64   /* sd_ngram_verify filler ids per pass; filler_k itself may be
+                                    anything up to vocab (ABI 11: one more launch pair per 64)  */
 
 typedef enum {
     SD_OK = 0,
@@ -354,7 +355,7 @@ typedef struct {
     sd_processor proc;           /* the loop's logits_processor                                */
     const int64_t* stop_tokens;
     int32_t n_stop;
-    int32_t filler_k;            /* 0..SD_NGRAM_MAX_FILLER                                     */
+    int32_t filler_k;            /* 0..vocab (ABI 11; p.topk(filler_top_k), any k)             */
     sd_noise noise;
     /* outputs, device */
     int32_t* n_accepted;         /* [B] n                                                      */

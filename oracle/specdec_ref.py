@@ -77,6 +77,10 @@ class Processor:
     # CPU), so WHICH of several equal logits at the cut survive is implementation-defined.
     # stable_ties=True keeps them lowest-index first (the HIP kernel's rule; same count).
     stable_ties: bool = False
+    # A user subclass's own _process (utils/logits_processor.py:18-20, the protocol's extension
+    # point): when set, processed_logits runs it (on a copy) instead of the kind's rule, and `kind`
+    # names only the sampling rule (greedy / multinomial).  tests/custom_procs.py builds these.
+    pre: Optional[Callable[[torch.Tensor], torch.Tensor]] = None
 
     @property
     def stochastic(self) -> bool:
@@ -118,6 +122,8 @@ def _mask_outside_nucleus(x: torch.Tensor, top_p: float, exact: bool = False,
 def processed_logits(logits: torch.Tensor, proc: Processor, exact: bool = False) -> torch.Tensor:
     """``LogitsProcessor._process`` on a copy (the reference's top-k mutates in place)."""
     x = logits.clone()
+    if proc.pre is not None:
+        return proc.pre(x)
     if proc.kind in ("topk", "topknucleus"):
         x = _mask_below_kth(x, proc.top_k)
     if proc.kind in ("nucleus", "topknucleus"):

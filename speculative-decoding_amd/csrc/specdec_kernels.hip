@@ -140,6 +140,9 @@ struct Plan {
     int64_t* filler_ids;
     int64_t filler_stride;
     int32_t filler_k;
+    int32_t filler_pass;    // filler top-K in passes of kNgMaxK: this launch's pass (> 0: filler only)
+    int32_t filler_kp;      //   ids this pass selects, <= kNgMaxK
+    float2* ng_thr;         //   per row: the last id the previous pass took (value, index bits)
 };
 
 // Phase timestamps (diagnostic builds, -DSD_PHASE_TIMING): thread 0 of workgroup `wg` records
@@ -3596,7 +3599,9 @@ int32_t launch_fused(const sd::Plan& P, void* stream) {
 // The fused verify's work layout for F (n_samp set): block-id order when the spans and deciders are
 // resident at once with headroom (the deciders poll the spans; the samplers, after them in dispatch
 // order, wait only for decisions and take freed slots) and the batch is small; otherwise ticket
-// order (stats_body, fused_role) with spans of kTicketSpan elements — at any batch, resident or not.
+// order (stats_body, fused_role) — at any batch, resident or not.  (From kTicketMinB sequences every
+// perf-mode verify streams spans of kTicketSpan elements, sd_verify: the fused and the two-launch
+// kernels then take the same row statistics, so their outputs stay identical.)
 // SD_OPT_FUSED_TICKET: -1 auto, 0 never (a non-resident grid then takes the two launches), 1 always.
 // false: no fused launch for this batch.
 constexpr int kTicketMinB = 64;
@@ -3609,9 +3614,6 @@ bool fused_layout(sd::Plan& F) {
     F.ticket = tmode == 1 || (tmode < 0 && (F.B >= kTicketMinB || !resident));
     if (!F.ticket) return resident;
     if (cap <= 0) return false;
-    F.chunk = kTicketSpan;
-    F.n_chunks = (F.V + F.chunk - 1) / F.chunk;
-    if (F.n_chunks > kWave) return false;
     const int per_unit = F.n_tslots * F.n_chunks + 1 + F.n_samp;
     F.lag = cap / per_unit;
     F.lag = F.lag < 1 ? 1 : (F.lag > F.B ? F.B : F.lag);
@@ -4089,6 +4091,12 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
     // the rows k_stats streams; at least 8 stages per workgroup: few rows (batch 1) then take 8 spans
     // per row instead of 63 one-stage ones (configs[1] multinomial 36.1 -> 33.7 us per step)
     set_stats_chunks(P, P.B * P.stat_slots, 512, 8);
+    if (a->noise.mode != SD_NOISE_STREAM && P.B >= kTicketMinB && P.chunk > kTicketSpan) {
+        // large perf-mode batches: 4 spans per Llama-3 row instead of one workgroup per row (set_stats_
+        // chunks' 512-workgroup target) — the ticket-order fused verify's layout, for both verify paths
+        P.chunk = kTicketSpan;
+        P.n_chunks = (P.V + P.chunk - 1) / P.chunk;
+    }
     Carve c{static_cast<char*>(a->workspace)};
     carve(P, c, a->batch * (2 * a->gamma + 1), a->batch, a->gamma, a->vocab);
 

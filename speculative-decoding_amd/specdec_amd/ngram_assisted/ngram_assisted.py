@@ -45,8 +45,8 @@ def ngram_assisted_speculative_generate(
     if torch.device(dev).type != "cuda":
         raise RuntimeError("specdec_amd.ngram_assisted_speculative_generate runs on the GPU (HIP); the target "
                            f"is on {dev}. There is no CPU path.")
-    if not 0 <= filler_top_k <= _lib.SD_NGRAM_MAX_FILLER:
-        raise ValueError(f"filler_top_k must be in [0, {_lib.SD_NGRAM_MAX_FILLER}]")
+    if filler_top_k < 0:   # any k up to the vocabulary (p.topk(k), ngram_assisted.py:152-155); ops checks V
+        raise ValueError("filler_top_k must be >= 0")
     stops = eos_tokens_id if isinstance(eos_tokens_id, list) else [eos_tokens_id]
     stop_t = torch.tensor(stops, dtype=torch.long, device=dev)
     accepted, speculated = 0.0, 0.0

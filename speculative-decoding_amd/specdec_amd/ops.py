@@ -49,34 +49,75 @@ class ProcSpec:
 PLAIN_SOFTMAX = ProcSpec("multinomial", 1.0)   # engine/infer_engine.py:241,276 (T=1, no processor)
 
 
-# the processor protocol's behaviour (utils/logits_processor.py:7-23): a subclass that redefines one
-# of these computes something the kernels do not, so it is refused, never run as its base class
-_PROC_BEHAVIOUR = ("__call__", "_process", "sample")
+# the processor protocol's behaviour (utils/logits_processor.py:7-23): a subclass that redefines the
+# softmax or the sampling rule computes something the kernels do not, so it is refused, never run as
+# its base class.  _process is the protocol's extension point: a subclass's own _process runs as it
+# is (torch ops on the device rows) and the kernels take its output (_user_process).
+_PROC_REFUSED = ("__call__", "sample")
+
+
+def _known_base(proc):
+    """(index in the MRO, name) of the first of the five processor classes proc derives from."""
+    mro = type(proc).__mro__
+    for i, cls in enumerate(mro):
+        if cls.__name__ in _CLASS_KIND:
+            return i, cls.__name__
+    return -1, type(proc).__name__
+
+
+def _user_process(proc):
+    """The bound ``_process`` of a user subclass of one of the five processors that overrides it (the
+    reference's extension point, utils/logits_processor.py:18-20), else None."""
+    if isinstance(proc, ProcSpec):
+        return None
+    i, _ = _known_base(proc)
+    if i <= 0:
+        return None
+    return proc._process if any("_process" in vars(sub) for sub in type(proc).__mro__[:i]) else None
 
 
 def proc_spec(proc) -> ProcSpec:
     """ProcSpec of one of the five processors (ours, the reference's, or a ProcSpec).
 
-    A subclass of a known processor is accepted only if it changes no behaviour (e.g. a constructor
-    that fixes parameters); one that overrides ``__call__``, ``_process`` or ``sample`` raises
-    TypeError — the kernels fuse the five processors' arithmetic and cannot run user code."""
+    A subclass of a known processor may override ``_process`` (its own processing — often
+    ``super()._process`` plus more): the rows are then processed by running it (``processed_rows``)
+    and the kernels apply the base class's sampling rule to them — softmax(y / T), then argmax
+    (GreedyProcessor) or the multinomial draw.  A subclass that overrides ``__call__`` or ``sample``
+    raises TypeError: the kernels fuse the softmax and the draw and cannot run user code there."""
     if isinstance(proc, ProcSpec):
         return proc
-    name = type(proc).__name__
-    mro = type(proc).__mro__
-    for i, cls in enumerate(mro):
-        if cls.__name__ in _CLASS_KIND:
-            name = cls.__name__
-            for sub in mro[:i]:
-                over = [m for m in _PROC_BEHAVIOUR if m in vars(sub)]
-                if over:
-                    raise TypeError(f"unsupported logits processor {type(proc).__name__}: {sub.__name__} overrides "
-                                    f"{', '.join(over)} of {name}, which the fused kernels cannot run")
-            break
-    if name not in _CLASS_KIND:
+    i, name = _known_base(proc)
+    if i < 0:
         raise TypeError(f"unsupported logits processor {type(proc).__name__}")
-    return ProcSpec(_CLASS_KIND[name], float(getattr(proc, "temperature", 1.0)),
-                    int(getattr(proc, "top_k", 0)), float(getattr(proc, "top_p", 1.0)))
+    mro = type(proc).__mro__
+    for sub in mro[:i]:
+        over = [m for m in _PROC_REFUSED if m in vars(sub)]
+        if over:
+            raise TypeError(f"unsupported logits processor {type(proc).__name__}: {sub.__name__} overrides "
+                            f"{', '.join(over)} of {name}, which the fused kernels cannot run")
+    T = float(getattr(proc, "temperature", 1.0))
+    if _user_process(proc) is not None:   # user processing: only the base's sampling rule stays fused
+        return ProcSpec("greedy" if name == "GreedyProcessor" else "multinomial", T)
+    return ProcSpec(_CLASS_KIND[name], T, int(getattr(proc, "top_k", 0)), float(getattr(proc, "top_p", 1.0)))
+
+
+def processed_rows(proc, rows):
+    """The rows the kernels read for processor ``proc``: the rows themselves, or — for a subclass
+    with its own ``_process`` — its output on a copy of each row (device torch ops; the caller's
+    logits are never modified).  rows: a tensor [R, V] or a sequence of them."""
+    fn = _user_process(proc)
+    if fn is None:
+        return rows
+
+    def one(t):
+        y = fn(t.clone())
+        if not torch.is_tensor(y) or y.shape != t.shape or y.device != t.device:
+            raise ValueError(f"{type(proc).__name__}._process must return a tensor of the input's shape and device")
+        if y.dtype not in _DT:
+            y = y.float()
+        return y if y.stride(-1) == 1 else y.contiguous()
+
+    return one(rows) if torch.is_tensor(rows) else [one(t) for t in rows]
 
 
 # sequences one Philox call verifies / samples (the arrival-counter block, kCntMax in the kernels)
@@ -186,6 +227,8 @@ def sample_rows(logits: torch.Tensor, proc, noise, tokens_out: Optional[torch.Te
     spec = proc_spec(proc)
     R, V = logits.shape
     _require_rows(logits, "logits", V)
+    logits = processed_rows(proc, logits)
+    proc = spec
     dev = logits.device
     shards = _row_shards(R, noise)
     if shards is not None:   # more rows than one call holds: row shards, one noise offset
@@ -228,7 +271,7 @@ def probs_rows(logits: torch.Tensor, proc) -> torch.Tensor:
     """LogitsProcessor.__call__: softmax(_process(logits) / T) in the logits dtype, on the device."""
     spec = proc_spec(proc)
     shape = logits.shape
-    x = logits.reshape(-1, shape[-1])
+    x = processed_rows(proc, logits.reshape(-1, shape[-1]))
     if x.stride(-1) != 1:
         x = x.contiguous()
     R, V = x.shape
@@ -287,6 +330,11 @@ def verify(target_rows: Sequence[torch.Tensor], draft_rows: Sequence[torch.Tenso
         # the batch-1 rule has no finished rows and no engine state (sampling/speculative_decoding.py:
         # 129-171); refused on every path, so a γ > SD_MAX_GAMMA window cannot drop them silently
         raise ValueError("active / engine_state belong to the ENGINE rule (SD_RULE_ENGINE)")
+    # user _process overrides: the kernels read the processed rows (processed_rows)
+    target_rows = processed_rows(target_proc, list(target_rows))
+    if not draft_is_probs:
+        draft_rows = processed_rows(draft_proc, list(draft_rows))
+    target_proc, draft_proc = proc_spec(target_proc), proc_spec(draft_proc)
     if gamma > _lib.SD_MAX_GAMMA:   # the reference takes any γ: windows of <= SD_MAX_GAMMA drafts (chunked.py)
         if prof_events is not None:
             raise ValueError("prof_events needs gamma <= SD_MAX_GAMMA")
@@ -437,9 +485,11 @@ def ngram_verify(target_rows: Sequence[torch.Tensor], draft_tokens: Optional[tor
     draft_tokens: int64 [B, >=γ'] (None when γ' == 0).  Under StreamNoise the torch generator
     advances by the words the draws consumed (the reference's order), one device->host read."""
     spec = proc_spec(proc)
+    target_rows = processed_rows(proc, list(target_rows))   # a user _process override (processed_rows)
+    proc = spec
     gamma = len(target_rows) - 1
-    if not 0 <= filler_k <= _lib.SD_NGRAM_MAX_FILLER:
-        raise ValueError(f"filler_k must be in [0, {_lib.SD_NGRAM_MAX_FILLER}]")
+    if not 0 <= filler_k <= target_rows[0].shape[-1]:   # p.topk(k) raises for k > V as well
+        raise ValueError(f"filler_k must be in [0, vocab = {target_rows[0].shape[-1]}]")
     if gamma > _lib.SD_MAX_GAMMA:   # the reference takes any γ: windows of <= SD_MAX_GAMMA drafts (chunked.py)
         from .chunked import ngram_verify_chunked
         return ngram_verify_chunked(target_rows, draft_tokens, proc, noise, stop_tokens, filler_k, sync_noise,

@@ -74,6 +74,11 @@ SPEC_CASES = [
     ("multi_t1_g48_bf16_close_eos", 4096, "bf16", 48, ("multinomial", 1.0, 0, 1.0), 200, "likely", False,
      [0, 1], 0.05),
     ("multi_t1_g40_bf16", 4096, "bf16", 40, ("multinomial", 1.0, 0, 1.0), 100, [1], False, [0]),
+    # user processors overriding only _process (tests/custom_procs.py, on the reference's classes)
+    ("custom_penalty_g4_bf16", 4096, "bf16", 4, ("custom:penalty", 1.0, 0, 1.0), 40, [1], False, [0, 1]),
+    ("custom_banned_topk_t08_g4_bf16", 4096, "bf16", 4, ("custom:banned_topk", 0.8, 50, 1.0), 40, [1], False, [0]),
+    ("custom_sharpen_greedy_g4_bf16", 4096, "bf16", 4, ("custom:sharpen_greedy", 1.0, 0, 1.0), 40, [1], False, [0]),
+    ("custom_penalty_g4_fp32", 4096, "fp32", 4, ("custom:penalty", 0.7, 0, 1.0), 40, [1], False, [0]),
 ]
 
 # The engine re-feeds the last prompt token to the drafter after its prefill (engine/infer_engine.py:206,231),
@@ -122,6 +127,11 @@ NGRAM_CASES = [
     ("ng_greedy_g40_n3", 4096, "bf16", ("multi", 3), 40, ("greedy", 1.0, 0, 1.0), 3, False, 160, [1], [0, 1]),
     ("ng_multi_g48_n3_f16", 4096, "bf16", ("multi", 3), 48, ("multinomial", 1.0, 0, 1.0), 16, False, 160, [1],
      [0, 1]),
+    ("ng_custom_penalty_g4_n3", 4096, "bf16", ("multi", 3), 4, ("custom:penalty", 1.0, 0, 1.0), 3, False, 40, [1],
+     [0, 1]),
+    # filler top-k beyond one 64-id pass (sd_ngram_verify runs a pass per 64 ids)
+    ("ng_multi_g4_n3_f128", 4096, "bf16", ("multi", 3), 4, ("multinomial", 1.0, 0, 1.0), 128, False, 40, [1], [0, 1]),
+    ("ng_greedy_g8_n3_f200", 4096, "bf16", ("multi", 3), 8, ("greedy", 1.0, 0, 1.0), 200, False, 40, [1], [0]),
 ]
 
 DT = {"bf16": torch.bfloat16, "fp32": torch.float32}
@@ -149,6 +159,9 @@ def prompt_for(V: int, seed: int, length: int = 8, batch: int = 1):
 
 
 def make_processor(lp, kind, T, k, p):
+    if kind.startswith("custom:"):   # a user subclass overriding _process (tests/custom_procs.py)
+        from custom_procs import make_custom
+        return make_custom(lp, kind.split(":", 1)[1], T, k, p)
     return {"greedy": lambda: lp.GreedyProcessor(T),
             "multinomial": lambda: lp.MultinomialProcessor(T),
             "topk": lambda: lp.TopKProcessor(T, k),

@@ -111,6 +111,7 @@ SPEC_GRID = [
 
 
 from parity_stats import DIVERGENCES, NUCLEUS_ROWS, TIE_DIVERGENCES  # noqa: E402
+from custom_procs import golden_processor  # noqa: E402
 
 
 def run_spec_oracle(tl, dl, ids, proc, gen, stops, skip=False, exact=False):
@@ -458,12 +459,10 @@ with open(os.path.join(GOLD, "engine_loops.json")) as f:
 
 
 def make_proc(sd, pp):
+    """The record's processor on the drop-in classes (custom:* = a user _process override,
+    tests/custom_procs.py)."""
     from specdec_amd.utils import logits_processor as lp
-    return {"greedy": lambda: lp.GreedyProcessor(pp["temperature"]),
-            "multinomial": lambda: lp.MultinomialProcessor(pp["temperature"]),
-            "topk": lambda: lp.TopKProcessor(pp["temperature"], pp["top_k"]),
-            "nucleus": lambda: lp.NucleusProcessor(pp["temperature"], pp["top_p"]),
-            "topknucleus": lambda: lp.TopKNucleusProcessor(pp["temperature"], pp["top_k"], pp["top_p"])}[pp["kind"]]()
+    return golden_processor(lp, pp)
 
 
 @pytest.mark.parametrize("case", sorted(SPEC))
@@ -480,8 +479,7 @@ def test_speculative_generate_matches_reference(sd, case):
         tc, dc = make_pair(c["vocab"], dtype=DT[c["dtype"]], sigma=c.get("sigma", 1.0))
         pp = c["processor"]
         match = []
-        for label, pv, exact in oracle_variants(ref.Processor(pp["kind"], pp["temperature"], pp["top_k"],
-                                                              pp["top_p"]))[1:]:
+        for label, pv, exact in oracle_variants(golden_processor(ref, pp))[1:]:
             torch.manual_seed(c["seed"])
             want = ref.speculative_generate(c["prompt"], dc, tc, gamma=c["gamma"], proc=pv,
                                             max_gen_len=c["max_gen_len"], eos_tokens_id=eos,
@@ -633,16 +631,12 @@ def test_ngram_loop_matches_reference(sd, case, store_kind):
                                             OneLevelNGramStorage, ngram_assisted_speculative_generate)
     if store_kind == "device":
         NGramStorage, OneLevelNGramStorage = DeviceNGramStorage, DeviceOneLevelNGramStorage   # noqa: N806
-    from specdec_amd.utils.logits_processor import (GreedyProcessor, MultinomialProcessor, NucleusProcessor,
-                                                    TopKProcessor)
+    from specdec_amd.utils import logits_processor as lp
     c = NGRAM_GOLDEN[case]
     DTm = {"bf16": torch.bfloat16, "fp32": torch.float32}
     target, _ = make_pair(c["vocab"], dtype=DTm[c["dtype"]], device=DEV, pos_mult=c["pos_mult"], peak=c["peak"])
     pp = c["processor"]
-    proc = {"greedy": lambda: GreedyProcessor(pp["temperature"]),
-            "multinomial": lambda: MultinomialProcessor(pp["temperature"]),
-            "topk": lambda: TopKProcessor(pp["temperature"], pp["top_k"]),
-            "nucleus": lambda: NucleusProcessor(pp["temperature"], pp["top_p"])}[pp["kind"]]()
+    proc = golden_processor(lp, pp)
     store = (NGramStorage if c["storage"] == "multi" else OneLevelNGramStorage)(c["n"], c["vocab"])
     eos = c["eos"] if len(c["eos"]) > 1 else c["eos"][0]
     torch.manual_seed(c["seed"])
@@ -653,7 +647,7 @@ def test_ngram_loop_matches_reference(sd, case, store_kind):
     if out != c["tokens"] or rate != c["acceptance_rate"]:
         # a torch-CPU rounding flip: then the exact-arithmetic oracle must agree
         cpu_target, _ = make_pair(c["vocab"], dtype=DTm[c["dtype"]], pos_mult=c["pos_mult"], peak=c["peak"])
-        kp = ref.Processor(pp["kind"], pp["temperature"], pp["top_k"], pp["top_p"], stable_ties=True)
+        kp = dataclasses.replace(golden_processor(ref, pp), stable_ties=True)
         torch.manual_seed(c["seed"])
         noise = ref.TorchNoise(None)
         st = ref.NgramStore(c["storage"], c["n"], c["vocab"], noise)

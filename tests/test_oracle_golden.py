@@ -6,6 +6,8 @@ from types import SimpleNamespace
 import pytest
 import torch
 
+from custom_procs import golden_processor
+
 from fakelm import make_pair, bank_digest
 from oracle import specdec_ref as ref
 
@@ -35,7 +37,7 @@ def test_spec_loop_matches_reference(case):
     target, drafter = pair(c["vocab"], c["dtype"], sigma=c.get("sigma", 1.0))
     assert bank_digest(target) == c["target_digest"] and bank_digest(drafter) == c["drafter_digest"]
     pp = c["processor"]
-    proc = ref.Processor(pp["kind"], pp["temperature"], pp["top_k"], pp["top_p"])
+    proc = golden_processor(ref, pp)
     eos = c["eos"] if len(c["eos"]) > 1 else c["eos"][0]
     torch.manual_seed(c["seed"])
     out, rate = ref.speculative_generate(c["prompt"], drafter, target, gamma=c["gamma"], proc=proc,
@@ -52,7 +54,7 @@ def test_ngram_loop_matches_reference(case):
     target, _ = make_pair(c["vocab"], dtype=DT[c["dtype"]], pos_mult=c["pos_mult"], peak=c["peak"])
     assert bank_digest(target) == c["target_digest"]
     pp = c["processor"]
-    proc = ref.Processor(pp["kind"], pp["temperature"], pp["top_k"], pp["top_p"])
+    proc = golden_processor(ref, pp)
     eos = c["eos"] if len(c["eos"]) > 1 else c["eos"][0]
     torch.manual_seed(c["seed"])
     noise = ref.TorchNoise(None)
