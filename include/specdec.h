@@ -296,6 +296,8 @@ typedef enum {
     SD_OPT_DRAW_SPAN = 6,       /* ABI 11. 0 (default): k_draw_lean's span per workgroup chosen by
                                    the batch (2048 elements, more for large batches); 1 / 2 / 4:
                                    that many 2048-element stages per workgroup                    */
+    SD_OPT_TICKET_LAG = 7,      /* ABI 11. 0 (default, 2): in the ticket-order fused verify, how many
+                                   sequences of a label stream before an earlier one's samplers  */
 } sd_option;
 int32_t sd_set_option(int32_t option, int32_t value);
 int32_t sd_get_option(int32_t option, int32_t* value);

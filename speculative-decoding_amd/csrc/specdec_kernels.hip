@@ -116,8 +116,9 @@ struct Plan {
     uint4* crec;          // fused verify, split records: the chunks' candidates, apart from their totals
     int32_t n_samp;       // fused verify (k_stats<.., SAMP>): sampling workgroups per sequence
     int32_t ticket;       // fused verify, any batch: work items by arrival ticket (fused_role), not block id
-    int32_t lag;          //   ticket mode: sequence b's samplers come after sequence b + lag's spans
-    uint32_t* ticket_ctr; //   ticket mode: the launch's ticket counter (zero between launches)
+    int32_t lag;          //   ticket mode: a sequence's samplers come after the spans of the label's lag-th next
+    int32_t labels;       //   ticket mode: label = block id % labels, one ticket counter and one sequence set each
+    uint32_t* ticket_ctr; //   ticket mode: the labels' ticket counters (kCntStride apart; zero between launches)
     int32_t* keep_hist;   // threshold scratch
     uint32_t* thr_part;   // 16-bit thresholds (sd_threshold.inc): per (row, slice) max key | NaN-inf flag
     float* thr_tail;      //   per (row, slice) Σexp below the window / tie counts
@@ -422,28 +423,29 @@ __device__ __forceinline__ void affine_split(int id, int per_seq, int& b, int& i
     item = k % per_seq;
 }
 
-// Ticket mode's schedule (stats_body): units u = 0 .. B + lag - 1; unit u holds sequence u's
-// per_seq items (its spans, then its decider) when u < B, then sequence (u - lag)'s n_samp
-// samplers when u >= lag.  Ticket t -> (sequence b, item) or (sequence b, sampler samp).
-__device__ __forceinline__ void fused_role(const Plan& P, int t, int per_seq, int& b, int& item, int& samp) {
-    const int D = P.lag, ns = P.n_samp, full = per_seq + ns;
+// Ticket mode's schedule within one label (stats_body) over its nb sequences j = 0 .. nb-1: units
+// u = 0 .. nb + D - 1; unit u holds sequence u's per_seq items (its spans, then its decider) when
+// u < nb, then sequence (u - D)'s ns samplers when u >= D.  Ticket t -> (sequence j, item) or
+// (sequence j, sampler samp).
+__device__ __forceinline__ void fused_role(int t, int nb, int D, int per_seq, int ns, int& j, int& item, int& samp) {
+    const int full = per_seq + ns;
     samp = -1;
     item = 0;
-    if (t < D * per_seq) {                       // units 0 .. lag-1: spans and deciders only
-        b = t / per_seq;
-        item = t - b * per_seq;
+    if (t < D * per_seq) {                       // units 0 .. D-1: spans and deciders only
+        j = t / per_seq;
+        item = t - j * per_seq;
         return;
     }
     t -= D * per_seq;
-    if (t < (P.B - D) * full) {                  // units lag .. B-1: both
+    if (t < (nb - D) * full) {                   // units D .. nb-1: both
         const int u = t / full, k = t - u * full;
-        if (k < per_seq) { b = D + u; item = k; }
-        else { b = u; samp = k - per_seq; }
+        if (k < per_seq) { j = D + u; item = k; }
+        else { j = u; samp = k - per_seq; }
         return;
     }
-    t -= (P.B - D) * full;                       // units B .. B+lag-1: samplers only
+    t -= (nb - D) * full;                        // units nb .. nb+D-1: samplers only
     const int u = t / ns;
-    b = P.B - D + u;
+    j = nb - D + u;
     samp = t - u * ns;
 }
 
@@ -484,25 +486,35 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     int samp = -1;
     if (SAMP && P.ticket) {
         // Ticket mode (any batch; the grid need not be resident): a workgroup's work item is the
-        // arrival ticket it takes, not its block id.  Every wait points at an EARLIER ticket — a
-        // decider at its spans, a sampler at its decider — whose holder is already running, so the
-        // launch always progresses whatever else holds the CUs; the one wait on later tickets (a
-        // decider for its samplers, `lag` sequences on) holds at most lag + 1 workgroups.  The items
-        // run sequence by sequence — spans, decider — with sequence b's samplers after sequence
-        // b + lag's items (fused_role): by then b's decision is about out, so samplers do not sit in
-        // slots the spans stream with, and they re-read the decided target row while the Infinity
-        // Cache still holds it.
+        // arrival ticket it takes, not its block id.  The sequences are dealt to `labels` labels
+        // (b % labels), and a workgroup serves the label of its block id (id % labels: with labels a
+        // multiple of 8 every workgroup of a label — so every item of a sequence — shares one XCD,
+        // whose L2 then serves the samplers' re-read of the decided rows), taking the next ticket of
+        // that label's own counter (one counter for the whole grid serialised its ~B*49 atomics: 92
+        // vs 49 us at B = 128).  Every wait points at an EARLIER ticket of the same label — a decider
+        // at its spans, a sampler at its decider — whose holder is already running, so the launch
+        // always progresses whatever else holds the CUs; the one wait on later tickets (a decider for
+        // its samplers, `lag` sequences on) holds at most lag + 1 workgroups per label.  A label's
+        // items run sequence by sequence — spans, decider — with a sequence's samplers after the
+        // spans of the label's lag-th next sequence (fused_role), so they rarely sit in slots waiting.
+        // Each label has the same workgroup count (ceil(B / labels) sequences' worth); a ticket past
+        // the label's real work exits.
+        const int NL = P.labels, L = (int)(blockIdx.x % (uint32_t)NL);
+        const int nbl = (P.B + NL - 1) / NL, nb = (P.B - L + NL - 1) / NL;
         __shared__ uint32_t s_tk;
         if (threadIdx.x == 0) {
-            const uint32_t t = __hip_atomic_fetch_add(P.ticket_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // the launch's last ticket: every other has been taken, re-arm the counter
-            if (t + 1u == (uint32_t)P.B * (uint32_t)(per_seq + P.n_samp))
-                __hip_atomic_store(P.ticket_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            uint32_t* ctr = P.ticket_ctr + (size_t)L * kCntStride;
+            const uint32_t t = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // the label's last ticket: every other has been taken, re-arm the counter
+            if (t + 1u == (uint32_t)nbl * (uint32_t)(per_seq + P.n_samp))
+                __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_tk = t;
         }
         __syncthreads();
-        int item;
-        fused_role(P, (int)s_tk, per_seq, b, item, samp);
+        if ((int)s_tk >= nb * (per_seq + P.n_samp)) return;   // padding: this label has fewer sequences
+        int item, j;
+        fused_role((int)s_tk, nb, P.lag < nb ? P.lag : nb, per_seq, P.n_samp, j, item, samp);
+        b = L + j * NL;
         decider = samp < 0 && item == n_span;
         s = slot_lo + (samp < 0 && item < n_span ? item / gx : 0);
         chunk = samp < 0 && item < n_span ? item % gx : 0;
@@ -3404,11 +3416,12 @@ void policy_init() {
 
 // Dispatch options (sd_set_option), indexed by sd_option; relaxed reads on every call.
 std::atomic<int> g_opt_fused{1}, g_opt_lean{-1}, g_opt_thr_poll{1}, g_opt_draw_stream{1}, g_opt_ticket{-1};
-std::atomic<int> g_opt_draw_span{0};
+std::atomic<int> g_opt_draw_span{0}, g_opt_ticket_lag{0};
 constexpr int kDrawSpan2MinB = 64, kDrawSpan4MinB = 256;   // k_draw_lean: batches above take 2 / 4 stages
 std::atomic<int>* option_slot(int32_t opt) {
     switch (opt) {
         case SD_OPT_DRAW_SPAN: return &g_opt_draw_span;
+        case SD_OPT_TICKET_LAG: return &g_opt_ticket_lag;
         case SD_OPT_FUSED_VERIFY: return &g_opt_fused;
         case SD_OPT_FUSED_TICKET: return &g_opt_ticket;
         case SD_OPT_LEAN_VERIFY: return &g_opt_lean;
@@ -3573,7 +3586,10 @@ int resident_cap(const void* kern, int threads, size_t dyn) {
 // samplers poll).  1 launched, 0 not applicable (the caller runs k_stats + k_sample), < 0 an error.
 template <int DT>
 int32_t launch_fused_dt(const sd::Plan& P, bool fast, void* stream) {
-    const int64_t head = (int64_t)P.B * (P.n_tslots * P.n_chunks + 1), total = head + (int64_t)P.B * P.n_samp;
+    const int64_t head = (int64_t)P.B * (P.n_tslots * P.n_chunks + 1);
+    // ticket mode: every label gets ceil(B / labels) sequences' workgroups (stats_body)
+    const int64_t seqs = P.ticket ? (int64_t)P.labels * ((P.B + P.labels - 1) / P.labels) : P.B;
+    const int64_t total = P.ticket ? seqs * (P.n_tslots * P.n_chunks + 1 + P.n_samp) : head + (int64_t)P.B * P.n_samp;
     if (!poll_allowed()) return 0;
     sd::Plan Q = P;
     Q.kpoll = 1;
@@ -3605,6 +3621,8 @@ int32_t launch_fused(const sd::Plan& P, void* stream) {
 // SD_OPT_FUSED_TICKET: -1 auto, 0 never (a non-resident grid then takes the two launches), 1 always.
 // false: no fused launch for this batch.
 constexpr int kTicketMinB = 64;
+constexpr int kTicketLabels = 64;   // labels (ticket counters) from B = 64; 8 below
+constexpr int kTicketLag = 2;       // default lag (SD_OPT_TICKET_LAG pins it)
 constexpr int kTicketSpan = 16 * kThreads * 8;   // 32768 elements: 4 spans per Llama-3 row
 bool fused_layout(sd::Plan& F) {
     const int cap = resident_cap(fused_kernel(F));
@@ -3615,10 +3633,14 @@ bool fused_layout(sd::Plan& F) {
     if (!F.ticket) return resident;
     if (cap <= 0) return false;
     const int per_unit = F.n_tslots * F.n_chunks + 1 + F.n_samp;
-    F.lag = cap / per_unit;
-    F.lag = F.lag < 1 ? 1 : (F.lag > F.B ? F.B : F.lag);
-    F.ticket_ctr = F.cnt + ((size_t)1 * kCntMax + (kCntMax - 1)) * kCntStride;   // set 1's last counter
+    F.labels = F.B >= kTicketLabels ? kTicketLabels : 8;
+    const int lg = opt(g_opt_ticket_lag);
+    F.lag = lg > 0 ? lg : kTicketLag;
+    // set 1's last `labels` counters (k_sample's arrivals of sequences B >= kCntMax - labels, which a
+    // call of that size only uses in counter mode, where they are zero between launches too)
+    F.ticket_ctr = F.cnt + ((size_t)1 * kCntMax + (kCntMax - F.labels)) * kCntStride;
     F.xcd_affine = 0;
+    (void)per_unit;
     return true;
 }
 
@@ -3990,6 +4012,7 @@ int32_t sd_set_option(int32_t option, int32_t value) {
     const bool ok = option == SD_OPT_FUSED_VERIFY ? (value >= 0 && value <= 2)
                   : option == SD_OPT_LEAN_VERIFY || option == SD_OPT_FUSED_TICKET ? (value >= -1 && value <= 1)
                   : option == SD_OPT_DRAW_SPAN ? (value == 0 || value == 1 || value == 2 || value == 4)
+                  : option == SD_OPT_TICKET_LAG ? (value >= 0 && value <= 64)
                                                  : (value == 0 || value == 1);
     if (!ok) return SD_ERR_INVALID;
     o->store(value, std::memory_order_relaxed);

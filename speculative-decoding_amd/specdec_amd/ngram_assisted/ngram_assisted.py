@@ -15,7 +15,7 @@ from torch.nn import Module
 
 from .. import _lib
 from ..noise import default_noise
-from ..ops import ngram_verify, proc_spec, sample_rows
+from ..ops import _user_process, ngram_verify, proc_spec, sample_rows
 from ..sampling.speculative_decoding import _forward
 from ..utils.caching import prune_cache
 from ..utils.logits_processor import GreedyProcessor, LogitsProcessor
@@ -40,6 +40,9 @@ def ngram_assisted_speculative_generate(
     debug: bool = False,
 ) -> Tuple[List[int], float]:
     spec = proc_spec(logits_processor)
+    # what the kernels are handed: the spec, or the processor itself when it has its own _process
+    # (ops.processed_rows runs it on the rows first)
+    kproc = logits_processor if _user_process(logits_processor) is not None else spec
     noise = default_noise()
     dev = target.device
     if torch.device(dev).type != "cuda":
@@ -68,7 +71,7 @@ def ngram_assisted_speculative_generate(
     if first_target:                                              # :78-93 (no stop check here)
         ids_d = torch.tensor([ids], dtype=torch.long, device=dev)
         logits, cache, _ = _forward(target, ids_d, cur, cache, use_cache)
-        tok, _, st = sample_rows(logits[:, -1, :], spec, noise)
+        tok, _, st = sample_rows(logits[:, -1, :], kproc, noise)
         t, bits = torch.stack([tok[0], st[0].long()]).tolist()
         _lib.raise_row_error(bits, "ngram_assisted_speculative_generate")   # torch raises (:89-90)
         ids[prompt_len] = t
@@ -95,7 +98,7 @@ def ngram_assisted_speculative_generate(
         ids_d = torch.tensor([drafted], dtype=torch.long, device=dev)
         logits, cache, start = _forward(target, ids_d, cur + g, cache, use_cache)   # :108-115
         rows = [logits[:, cur - 1 + t - start, :] for t in range(g + 1)]           # p rows and the bonus row
-        out = ngram_verify(rows, ids_d[:, cur:cur + g] if g else None, spec, noise, stop_t, filler_k=filler)
+        out = ngram_verify(rows, ids_d[:, cur:cur + g] if g else None, kproc, noise, stop_t, filler_k=filler)
         head = torch.stack([out.n_accepted[0].long(), out.next_token[0], out.row_status[0].long(),
                             out.stop_index[0].long()]).tolist()
         n, x, status, stop_index = (int(v) for v in head)

@@ -21,7 +21,7 @@ from torch.nn import Module
 
 from .. import _lib
 from ..noise import StreamNoise, default_noise, noise_session
-from ..ops import proc_spec, sample_rows, verify
+from ..ops import _user_process, proc_spec, sample_rows, verify
 from ..utils.caching import prune_cache
 from ..utils.logits_processor import GreedyProcessor, LogitsProcessor
 
@@ -96,6 +96,9 @@ def _static_caches(drafter, target, total_len):
 def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processor, max_gen_len, eos_tokens_id,
                           pad_token_id, use_cache, skip_sample_adjustment, first_target, debug, static_cache=False):
     spec = proc_spec(logits_processor)
+    # what the kernels are handed: the spec, or the processor itself when it has its own _process
+    # (ops.processed_rows runs it on the rows first)
+    kproc = logits_processor if _user_process(logits_processor) is not None else spec
     dev = target.device
     if torch.device(dev).type != "cuda":
         raise RuntimeError("specdec_amd.speculative_generate runs on the GPU (HIP); the target is on "
@@ -130,7 +133,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
     if first_target:                                             # :84-103
         logits, target_cache, _ = _forward(target, input_ids, cur, target_cache, use_cache, tlen if static else None)
         tlen = cur
-        sample_rows(logits[:, -1, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1], status_or=err)
+        sample_rows(logits[:, -1, :], kproc, noise, tokens_out=input_ids[0, cur:cur + 1], status_or=err)
         t, bits = torch.stack([input_ids[0, cur], err[0].long()]).tolist()
         _lib.raise_row_error(bits, "speculative_generate")
         cur += 1
@@ -157,7 +160,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
                 V = row.shape[-1]
                 noise.reserve(g * 2 * V + g + 2 * V, dev)
             tok = ids_d[0, cur + k:cur + k + 1]
-            sample_rows(row, spec, noise, tokens_out=tok, row_stats_out=dstats[k] if stash else None, status_or=err_d)
+            sample_rows(row, kproc, noise, tokens_out=tok, row_stats_out=dstats[k] if stash else None, status_or=err_d)
             tok.clamp_(0, row.shape[-1] - 1)   # a failed row's -1 never reaches a forward
             draft_rows.append(row if row.device == torch.device(dev) else row.to(dev))
         drafts_speculated += g
@@ -167,7 +170,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
         tlen = cur + g
         if g == 0:
             # last position: rand(0) draws nothing, n = 0 = γ', the bonus row is sampled (:158-171)
-            sample_rows(logits[:, cur - 1 - start, :], spec, noise, tokens_out=input_ids[0, cur:cur + 1],
+            sample_rows(logits[:, cur - 1 - start, :], kproc, noise, tokens_out=input_ids[0, cur:cur + 1],
                         status_or=err)
             check_err()
             x = int(input_ids[0, cur].item())
@@ -176,7 +179,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
                 return input_ids[0, prompt_len:cur].tolist(), drafts_accepted / drafts_speculated
             continue
         trows = [logits[:, cur - 1 + t - start, :] for t in range(g + 1)]   # :135 and bonus row :159
-        out = verify(trows, draft_rows, input_ids[:, cur:cur + g], _lib.SD_RULE_SPEC, spec, spec, noise,
+        out = verify(trows, draft_rows, input_ids[:, cur:cur + g], _lib.SD_RULE_SPEC, kproc, kproc, noise,
                      stop_t, skip_sample_adjustment=skip_sample_adjustment,
                      draft_row_stats=dstats[:g] if stash else None, status_or=err)
         if err_d is not err:

@@ -95,6 +95,14 @@ def expect_path(sd, out, B, draws, stochastic=True):
     assert out.path in want, sd.lib.PATH_NAMES.get(out.path)
 
 
+def flip_slack(logits_row, dtype):
+    """Σ over the row's elements of how far its rounded probability can move when the softmax
+    normaliser is off by 1e-6 (relative): the exact fp64 value, scaled by 1 ± 1e-6, rounded to the
+    row's dtype both ways."""
+    v = torch.softmax(logits_row.double(), dim=-1)
+    return float(((v * (1 + 1e-6)).to(dtype).double() - (v * (1 - 1e-6)).to(dtype).double()).sum())
+
+
 def chi2_check(samples, probs, label):
     """Pearson chi-square of integer samples against probabilities (bins with expected < 5 pooled)."""
     from scipy.stats import chisquare
@@ -246,7 +254,12 @@ def test_perf_engine_accept_walk_and_state(sd, B, V, dtype, draws):
             assert 0 <= x[b] < V
             expect[step + want] = x[b]
             res = (pt[b, want].double() - qf[b, want].double()).clamp(min=0)
-            assert abs(mass[b] - float(res.sum())) <= 1e-5
+            # 1e-5 (the north star's tolerance) plus what one-ulp rounding flips of p and q can move:
+            # the kernels' softmax normaliser is within ~1e-7 of the exact one, so an element whose
+            # exact probability lies within 1e-6 (relative) of a rounding boundary may round either
+            # way (at V = 32768, B = 512 such a flip of a large p moved one row's mass by 1.3e-5)
+            slack = flip_slack(tl[b, want], dtype) + flip_slack(dl[b, want], dtype)
+            assert abs(mass[b] - float(res.sum())) <= 1e-5 + slack, (b, mass[b], float(res.sum()), slack)
             assert float(res[x[b]]) > 0
             assert bool(fin_h[b]) == (x[b] in ends)
         else:
