@@ -188,7 +188,8 @@ class EngineStep:
         """STREAM: the step's words in one generation (γ draws of 2·B·V, the verify's <= B·(γ+2V)),
         as the drop-in engine reserves a window's words (noise.StreamNoise.reserve)."""
         if hasattr(self.noise, "reserve"):
-            self.noise.reserve(self.g * 2 * self.B * self.V + self.B * (self.g + 2 * self.V), self.trows[0].device)
+            self.noise.reserve(self.g * 2 * self.B * self.V + self.B * (self.g + 2 * self.V), self.trows[0].device,
+                               known=self.g * 2 * self.B * self.V)
 
     def __call__(self, prof=None):
         self.reserve()

@@ -71,7 +71,8 @@ class HotPathTimer:
             setattr(mod, name, fn)
 
 
-def run(batch=32, prompt=128, gen=64, gamma=4, layers_8b=32, layers_1b=16, modes=("philox", "stream")):
+def run(batch=32, prompt=128, gen=64, gamma=4, layers_8b=32, layers_1b=16,
+        modes=("philox", "stream", "philox_cached", "stream_cached")):
     """Build the two random-init models, run the drop-in engine once per noise mode (after a warm-up
     run) and return the report dict."""
     from specdec_amd import set_noise_mode
@@ -92,10 +93,14 @@ def run(batch=32, prompt=128, gen=64, gamma=4, layers_8b=32, layers_1b=16, modes
            "dtype": "bf16", "batch": batch, "prompt_len": prompt, "gen_len": gen,
            "gamma": gamma, "model_build_s": build_s,
            "note": "random weights: the acceptance rate is meaningless (near-uniform logits); the tokens/s and the "
-                   "hot path's share of the wall time are the measurement. The target runs uncached over the whole "
-                   "sequence every window, as the reference does (engine/infer_engine.py:270-273)."}
+                   "hot path's share of the wall time are the measurement. philox / stream: the target runs "
+                   "uncached over the whole sequence every window, as the reference does "
+                   "(engine/infer_engine.py:270-273); *_cached: the opt-in cached target window "
+                   "(ctx.cached_target: KV cache cropped to the previous window's start, same tokens)."}
     for mode in modes:
-        set_noise_mode(mode, seed=5) if mode == "philox" else set_noise_mode("stream")
+        noise_mode = mode.split("_")[0]
+        ctx.cached_target = mode.endswith("_cached")
+        set_noise_mode(noise_mode, seed=5) if noise_mode == "philox" else set_noise_mode("stream")
         torch.manual_seed(3)
         infer_engine.batch_speculative_generate(ctx, ids, mask, batch)   # warm-up
         torch.cuda.synchronize()

@@ -579,14 +579,26 @@ __device__ __forceinline__ float exp1_screen16(uint32_t hi, uint32_t lo) {
     return u < 9.765625e-04f ? u * fmaf(0.5f, u, 1.0f) : big;
 }
 
+// STREAM (ABI 11): word i of a call is words[stream_base(nz) + i], base = offset + *offset_dev (both
+// optional): a noise session hands every call its pool and the call's start inside it — the host
+// part (draws of known size) in `offset`, the part only the device knows (what the previous verify
+// consumed) in `offset_dev` — so a pool generated ahead, on another stream, needs no host sync.
+// n_words is the pool's capacity from words[0].
+__device__ __forceinline__ int64_t stream_base(const sd_noise& nz) {
+    return (int64_t)nz.offset + (nz.offset_dev ? (int64_t)*reinterpret_cast<const int64_t*>(nz.offset_dev) : 0);
+}
+__device__ __forceinline__ const uint32_t* stream_ptr(const sd_noise& nz) { return nz.words + stream_base(nz); }
+__device__ __forceinline__ int64_t stream_cap(const sd_noise& nz) { return nz.n_words - stream_base(nz); }
+
 // torch's exponential_ words of VEC consecutive elements (two per element, from woff + 2 e0): 16-byte
 // loads when aligned and in range, else per-word loads; words past the buffer read as 0 (the
 // callers flag the overrun).
 template <int VEC>
 __device__ __forceinline__ void stream_words(const sd_noise& nz, int64_t woff, int64_t e0, uint32_t* w) {
     const int64_t w0 = woff + 2 * e0;
-    const uint32_t* src = nz.words + w0;
-    if (w0 + 2 * VEC <= nz.n_words && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const uint32_t* src = stream_ptr(nz) + w0;
+    const int64_t cap = stream_cap(nz);
+    if (w0 + 2 * VEC <= cap && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
 #pragma unroll
         for (int q = 0; q < VEC / 2; ++q) {
             const uint4 t = reinterpret_cast<const uint4*>(src)[q];
@@ -594,7 +606,7 @@ __device__ __forceinline__ void stream_words(const sd_noise& nz, int64_t woff, i
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 2 * VEC; ++k) w[k] = w0 + k < nz.n_words ? src[k] : 0u;
+        for (int k = 0; k < 2 * VEC; ++k) w[k] = w0 + k < cap ? src[k] : 0u;
     }
 }
 
@@ -647,8 +659,9 @@ __device__ __forceinline__ float span_gumbel(const sd_noise& nz, uint32_t row, u
 __device__ __forceinline__ float exp_noise(const sd_noise& nz, int64_t woff, int row, int64_t j) {
     if (nz.mode == SD_NOISE_STREAM) {
         const int64_t w = woff + 2 * j;
-        if (w + 1 >= nz.n_words) return 1.f;   // overrun is flagged by the caller
-        return exp1_from_words(nz.words[w], nz.words[w + 1]);
+        if (w + 1 >= stream_cap(nz)) return 1.f;   // overrun is flagged by the caller
+        const uint32_t* ws = stream_ptr(nz);
+        return exp1_from_words(ws[w], ws[w + 1]);
     }
     const uint4 q = philox_block(nz, (uint32_t)row, kSiteSample, (uint32_t)(j >> 2));
     const uint32_t w = (j & 3) == 0 ? q.x : (j & 3) == 1 ? q.y : (j & 3) == 2 ? q.z : q.w;

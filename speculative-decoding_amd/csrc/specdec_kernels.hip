@@ -885,8 +885,8 @@ __global__ void __launch_bounds__(256) k_decide(Plan P) {
 // ------------------------------------------------------------------ walk
 __device__ __forceinline__ float draw_uniform(const Plan& P, int b, int i, int64_t woff, bool* overrun) {
     if (P.noise.mode == SD_NOISE_STREAM) {
-        if (woff >= P.noise.n_words) { *overrun = true; return 0.f; }
-        return uniform_from_word(P.noise.words[woff]);
+        if (woff >= stream_cap(P.noise)) { *overrun = true; return 0.f; }
+        return uniform_from_word(stream_ptr(P.noise)[woff]);
     }
     const uint4 q = philox_block(P.noise, (uint32_t)b, kSiteAccept, (uint32_t)(i >> 2));   // 4 drafts per block
     return uniform_from_word((i & 3) == 0 ? q.x : (i & 3) == 1 ? q.y : (i & 3) == 2 ? q.z : q.w);
@@ -968,7 +968,7 @@ __device__ Decision walk_core(const Plan& P, int b, const float* rp, const float
         }
     }
     if (overrun || (P.noise.mode == SD_NOISE_STREAM && d.mode != kModeNone && P.t_stoch &&
-                    d.noise_off + sample_words > P.noise.n_words))
+                    d.noise_off + sample_words > stream_cap(P.noise)))
         d.status |= SD_ROW_NOISE_OVERRUN;
     if (d.mode != kModeNone) {   // the sampled rows' stats travel with the decision (pick_wave reads them)
         d.mst = P.rowstat[b * P.slots + d.slot];
@@ -1043,14 +1043,16 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                 constexpr int kPer = kWalkWords / 256;
                 const float invW = 1.0f / (float)W;
                 const int nw = nb * W;
+                const uint32_t* pw = stream_ptr(P.noise);
+                const int64_t pcap = stream_cap(P.noise);
                 uint32_t wv[kPer];
 #pragma unroll
                 for (int q = 0; q < kPer; ++q) {
                     const int i = tid + q * 256;
                     const int k = (int)(((float)i + 0.5f) * invW), j = i - k * W;   // exact: i, W < 2^14
                     const int64_t w = off + V2 * k + j;
-                    const bool ok = i < nw && w < P.noise.n_words;
-                    wv[q] = P.noise.words[ok ? w : 0];
+                    const bool ok = i < nw && w < pcap;
+                    wv[q] = pw[ok ? w : 0];
                     wv[q] = ok ? wv[q] : 0u;
                 }
                 constexpr int kPerD = kWalkDrafts / 256;
@@ -1151,7 +1153,8 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                 Decision d = walk_core(P, b, lrp + bi * g, lrq + bi * g, woff, &used, true, accm, lstop + bi * g);
                 const bool sampled = spec ? (d.mode != kModeNone && P.t_stoch) : d.mode == kModeResid;
                 const int64_t n_u = used - (sampled ? V2 : 0);
-                for (int i = 0; i < n_u; ++i) ovr |= woff + i >= P.noise.n_words;
+                const int64_t cap = stream_cap(P.noise);
+                for (int i = 0; i < n_u; ++i) ovr |= woff + i >= cap;
                 if (ovr) d.status |= SD_ROW_NOISE_OVERRUN;
                 publish_decision(P, b, d);
             }
@@ -1514,7 +1517,7 @@ __device__ __forceinline__ void resid_body(const Plan& P, const Decision& d, int
                 stream_words<VEC>(P.noise, d.noise_off, e0, wd + 2 * v * VEC);
 #pragma unroll
                 for (int k = 0; k < VEC; ++k)
-                    e[k] = d.noise_off + 2 * (e0 + k) + 1 < P.noise.n_words
+                    e[k] = d.noise_off + 2 * (e0 + k) + 1 < stream_cap(P.noise)
                                ? exp1_fast_from_words(wd[2 * (v * VEC + k)], wd[2 * (v * VEC + k) + 1]) : 1.f;
             }
         } else {
@@ -1574,7 +1577,7 @@ __device__ __forceinline__ void resid_body(const Plan& P, const Decision& d, int
             const int slot = atomicAdd(&lcount, 1);
             if (slot < kMaxCand) {
                 if constexpr (NZ == SD_NOISE_STREAM)   // the exact value, for the candidates only
-                    if (stoch) ee = d.noise_off + 2 * j + 1 < P.noise.n_words ? exp1_from_words(h, l) : 1.f;
+                    if (stoch) ee = d.noise_off + 2 * j + 1 < stream_cap(P.noise) ? exp1_from_words(h, l) : 1.f;
                 lres[slot] = rr;
                 le[slot] = ee;
                 lidx[slot] = (int32_t)j;
@@ -2671,7 +2674,7 @@ __global__ void __launch_bounds__(64) k_sample_finalize(Plan P) {
         int32_t st = SD_ROW_DONE;
         if (P.t_stoch && !(ms.y > 0.f && ms.y < INFINITY)) st |= SD_ROW_INVALID_DIST;   // NaN / inf / zero mass
         if (P.t_keep) st |= keep_of(P, r).flags;
-        if (P.noise.mode == SD_NOISE_STREAM && P.t_stoch && 2ll * P.V * P.B > P.noise.n_words)
+        if (P.noise.mode == SD_NOISE_STREAM && P.t_stoch && 2ll * P.V * P.B > stream_cap(P.noise))
             st |= SD_ROW_NOISE_OVERRUN;
         // no candidate at all (an all-NaN / all -inf row: the race's threshold is NaN) is an invalid
         // distribution too; a failed row's token is -1, never an index a forward could be fed

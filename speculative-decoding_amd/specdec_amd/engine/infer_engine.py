@@ -244,6 +244,14 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
     # changes nothing, so the outputs are the reference's.  STREAM keeps the exact check: such a
     # window would still consume generator words.
     probe = _FinishedProbe(finished, err) if isinstance(noise, PhiloxNoise) else None
+    # Opt-in (ctx.cached_target = True): the target keeps a KV cache instead of re-encoding the whole
+    # sequence every window (:269-273).  A window's positions are final only after its verify (the
+    # rejected drafts are zeroed, :332-336), so the cache is cropped back to the start of the previous
+    # window and each forward feeds that window's final tokens plus the new drafts: the same token
+    # sequence and positions as the reference's full forward, its logits up to rounding.  Default: off
+    # (the reference's uncached forward).
+    cached = bool(getattr(ctx, "cached_target", False))
+    t_past, t_valid = None, 0                                             # cache and its valid length
     step = 0
     while step < gen_len:                                                 # :211
         if probe is not None:
@@ -269,7 +277,7 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
             if d == 0 and isinstance(noise, StreamNoise):
                 # the window's words in one generation: γ_w draws of 2·B·V, the verify's <= B·(γ_w + 2V)
                 V = logits.shape[-1]
-                noise.reserve(gw * 2 * B * V + B * (gw + 2 * V), dev)
+                noise.reserve(gw * 2 * B * V + B * (gw + 2 * V), dev, known=gw * 2 * B * V)
             samples, _, _ = sample_rows(logits, PLAIN_SOFTMAX, noise,     # :241-246 softmax + multinomial
                                         row_base=row_base, row_stats_out=dstats[d] if stash else None,
                                         status_or=err)
@@ -282,9 +290,16 @@ def _batch_speculative_generate(noise, ctx, input_ids, attention_mask, batch_siz
                 for idx in range(B):                                      # step 0: every row is active
                     first_token_callback(idx)
         verify_ids = torch.cat([input_ids, generated[:, :step + gw]], dim=1).to(target_device)  # :269-270
-        t_logits = ctx.target(verify_ids).logits                          # :273
-        L = t_logits.shape[1]
-        trows = [t_logits[:, L - gw - 1 + t, :] for t in range(gw)]      # :275 logits[:, -(γ+1):-1]
+        L = verify_ids.shape[1]
+        if cached:
+            if t_past is not None:
+                t_past.crop(t_valid)                                      # drop the previous window's drafts
+            out = ctx.target(verify_ids[:, t_valid:], past_key_values=t_past, use_cache=True)
+            t_logits, t_past, first = out.logits, out.past_key_values, t_valid
+            t_valid = L - gw                                              # this window is final after its verify
+        else:
+            t_logits, first = ctx.target(verify_ids).logits, 0           # :273
+        trows = [t_logits[:, L - gw - 1 + t - first, :] for t in range(gw)]   # :275 logits[:, -(γ+1):-1]
         if any(r.device != t_logits.device for r in rows):
             rows = [r.to(t_logits.device) for r in rows]
         verify(trows, rows, draft_tokens, _lib.SD_RULE_ENGINE, PLAIN_SOFTMAX, PLAIN_SOFTMAX, noise, stops,

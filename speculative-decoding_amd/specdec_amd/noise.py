@@ -35,6 +35,8 @@ _DEVICE_GEN = os.environ.get("SPECDEC_STREAM_DEVICE", "1") != "0"
 # smallest multiple of 64 Ki words that needs at most kMaxSubstreams substreams (an engine step's
 # 41 M words at B = 32, V = 128256: 192 Ki words, 209 substreams).  SPECDEC_MT_STRIDE pins it.
 _STRIDE_ENV = os.environ.get("SPECDEC_MT_STRIDE")
+# steps per pipelined pool (StreamNoise.reserve(..., known=...) in a session); 0 = no pipeline
+_PIPE_STEPS = int(os.environ.get("SPECDEC_STREAM_PIPELINE", "4"))
 MT_STRIDE = int(_STRIDE_ENV) if _STRIDE_ENV else 65536
 MT_MAX_SUBSTREAMS = 240
 
@@ -60,6 +62,142 @@ def jump_table(device, stride: int, count: int) -> torch.Tensor:
         t = torch.from_numpy(host.view(np.int64)).to(dev)
         _JUMP[key] = t
     return t
+
+
+def _mt_generate(state: torch.Tensor, words: torch.Tensor, n: int, ws_box: list, stream) -> None:
+    """sd_mt19937_generate: the n words after `state` into words[:n] on `stream` (ws_box[0]: a
+    workspace tensor grown in place, one per stream)."""
+    dev = words.device
+    stride = mt_stride(n)
+    S = (n + stride - 1) // stride
+    table = jump_table(dev, stride, max(S - 1, 1))
+    need = lib.sd_mt19937_generate_workspace_size(n, stride)
+    if ws_box[0] is None or ws_box[0].numel() < need:
+        ws_box[0] = torch.empty(need + need // 4, dtype=torch.uint8, device=dev)
+    a = _lib.sd_mt_generate_args(state.data_ptr(), table.data_ptr(), table.shape[0], stride, words.data_ptr(), n,
+                                 ws_box[0].data_ptr(), ws_box[0].numel())
+    _lib.check(lib.sd_mt19937_generate(C.byref(a), C.c_void_p(stream.cuda_stream)), "sd_mt19937_generate")
+
+
+def _mt_commit(state: torch.Tensor, words: torch.Tensor, n_generated: int, used: int, used_dev, stream) -> None:
+    """sd_mt19937_commit: move `state` past used + *used_dev of the n_generated words after it."""
+    _lib.check(lib.sd_mt19937_commit(state.data_ptr(), words.data_ptr(), n_generated,
+                                     used_dev.data_ptr() if used_dev is not None else None, int(used), None,
+                                     C.c_void_p(stream.cuda_stream)), "sd_mt19937_commit")
+
+
+class _Pool:
+    """One pipelined pool: `cap` generator words (+ 624 of slack for commits) from the position whose
+    generator state is `state`; `ready` is recorded on the generation stream once they are written."""
+
+    def __init__(self, words: torch.Tensor, cap: int):
+        self.words, self.cap = words, cap
+        self.state: Optional[torch.Tensor] = None
+        self.ready: Optional[torch.cuda.Event] = None
+        # the anchor, in the previous pool's coordinates: host part snap_host + K, device part a_dev
+        self.snap_host = 0
+        self.K = 0
+        self.a_dev: Optional[torch.Tensor] = None
+        self.dev_since = 0     # upper bound of the device-counted words since the anchor snapshot
+
+
+class _Pipeline:
+    """STREAM words generated ahead, on a side stream, while the calls consume the current pool
+    (DESIGN §4 "STREAM pool pipeline").  A session's steps (``reserve(n, known=...)``: n words at
+    most, `known` of them host-known — the draws) consume consecutive generator positions; the call
+    start inside the current pool is host_off + *rel_dev (the kernels add both, ABI 11), rel_dev
+    summing the verifies' device counts, so nothing is read back.  The next pool is generated from
+    an anchor no later than where the current pool will be left: the position at the switch into
+    the current pool plus the host-known words of `steps` steps; it holds `steps` + 1 steps' worst
+    case plus the verifies' slack, so the switch (after `steps` steps) always lands inside it and
+    the pool after it is generated meanwhile, on the side stream, behind an event."""
+
+    def __init__(self, dev: torch.device, state: torch.Tensor, n: int, known: int, steps: int):
+        self.dev = dev
+        self.steps = steps
+        self.n, self.known = n, known
+        self.cap = (steps + 1) * n + steps * (n - known)
+        self.side = torch.cuda.Stream(dev)
+        self.ws_main, self.ws_side = [None], [None]
+        bufs = [torch.empty(self.cap + 624, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.pools = [_Pool(b, self.cap) for b in bufs]
+        self.i = 0                                   # the current pool's buffer
+        cur = self.pools[0]
+        cur.state = state.clone()
+        main = torch.cuda.current_stream(dev)
+        _mt_generate(cur.state, cur.words, self.cap + 624, self.ws_main, main)   # the first pool: in line
+        self.host_off = 0
+        self.rel_dev = torch.zeros(1, dtype=torch.long, device=dev)
+        self.dev_hi = 0                              # upper bound of *rel_dev
+        self.nxt: Optional[_Pool] = None
+        self._enqueue_next()
+
+    @property
+    def cur(self) -> _Pool:
+        return self.pools[self.i]
+
+    def _enqueue_next(self) -> None:
+        """Generate the other buffer's pool on the side stream, anchored at host_off + K + *rel_dev
+        (snapshot) of the current pool, K = the host-known words of `steps` steps."""
+        main = torch.cuda.current_stream(self.dev)
+        nxt = self.pools[1 - self.i]
+        nxt.snap_host, nxt.K = self.host_off, self.steps * self.known
+        nxt.a_dev = self.rel_dev.clone()             # snapshot (stream-ordered on the main stream)
+        nxt.dev_since = 0
+        nxt.state = self.cur.state.clone()
+        snap = torch.cuda.Event()
+        snap.record(main)                            # also orders the buffer's last readers before it
+        self.side.wait_event(snap)
+        with torch.cuda.stream(self.side):
+            nxt.a_dev.record_stream(self.side)
+            nxt.state.record_stream(self.side)
+            _mt_commit(nxt.state, self.cur.words, self.cap + 624, nxt.snap_host + nxt.K, nxt.a_dev, self.side)
+            _mt_generate(nxt.state, nxt.words, self.cap + 624, self.ws_side, self.side)
+            nxt.ready = torch.cuda.Event()
+            nxt.ready.record(self.side)
+        self.nxt = nxt
+
+    def fits(self, n: int) -> bool:
+        return self.host_off + self.dev_hi + n <= self.cap
+
+    def switch(self, n: int) -> bool:
+        """Move to the next pool if the walk has passed its anchor and it holds n more words."""
+        nxt = self.nxt
+        if nxt is None or self.host_off < nxt.snap_host + nxt.K:
+            return False
+        new_host = self.host_off - nxt.snap_host - nxt.K
+        if new_host + nxt.dev_since + n > self.cap:
+            return False
+        main = torch.cuda.current_stream(self.dev)
+        main.wait_event(nxt.ready)
+        self.rel_dev.sub_(nxt.a_dev)                 # exact, on the device: >= 0, <= nxt.dev_since
+        self.host_off, self.dev_hi = new_host, nxt.dev_since
+        self.i = 1 - self.i
+        self.nxt = None
+        self._enqueue_next()
+        return True
+
+    def take(self, n: int):
+        """(pool words, host offset, device offset) for a call of up to n words, or None."""
+        if not self.fits(n) and not self.switch(n):
+            return None
+        return self.cur.words, self.host_off, self.rel_dev
+
+    def consumed(self, count: Optional[int], used_dev: Optional[torch.Tensor], worst: int) -> None:
+        if used_dev is None:
+            self.host_off += int(count or 0)
+        else:
+            self.rel_dev.add_(used_dev.view(1))
+            self.dev_hi += worst
+            if self.nxt is not None:
+                self.nxt.dev_since += worst
+
+    def final_state(self) -> torch.Tensor:
+        """The generator state after every consumed word (device; stream-ordered)."""
+        st = self.cur.state.clone()
+        _mt_commit(st, self.cur.words, self.cap + 624, self.host_off, self.rel_dev,
+                   torch.cuda.current_stream(self.dev))
+        return st
 
 
 class _DeviceMT:
@@ -133,12 +271,17 @@ class StreamNoise:
     """
     mode = _lib.SD_NOISE_STREAM
 
-    def __init__(self, generator: Optional[torch.Generator] = None, device_generation: Optional[bool] = None):
+    def __init__(self, generator: Optional[torch.Generator] = None, device_generation: Optional[bool] = None,
+                 pipeline_steps: Optional[int] = None):
         self.generator = generator
         self.device_generation = _DEVICE_GEN if device_generation is None else bool(device_generation)
         self._dev: Optional[_DeviceMT] = None
         self._depth = 0
         self._pool: Optional[Tuple[torch.Tensor, int]] = None   # (the reserved words, host cursor)
+        # steps per pipelined pool (reserve(..., known=...) inside a session); 0 turns the pipeline off
+        self.pipeline_steps = _PIPE_STEPS if pipeline_steps is None else int(pipeline_steps)
+        self._pipe: Optional[_Pipeline] = None
+        self._last_need = 0
 
     @property
     def gen(self) -> torch.Generator:
@@ -164,12 +307,40 @@ class StreamNoise:
     def _device_mt(self, dev: torch.device) -> _DeviceMT:
         if self._dev is None or self._dev.device != dev:
             if self._dev is not None:                   # moving devices mid-session: hand over
+                self._leave_pipeline()
                 self._close_pool()
                 self._dev.pull(self.gen)
             self._dev = _DeviceMT(dev, self.gen.get_state())
         return self._dev
 
-    def reserve(self, n_words: int, device) -> None:
+    def _leave_pipeline(self) -> None:
+        """Back to the per-call generation: the device state moves to where the pipeline stands."""
+        if self._pipe is None:
+            return
+        self._dev.state = self._pipe.final_state()
+        self._pipe = None
+
+    def reserve(self, n_words: int, device, known: Optional[int] = None) -> None:
+        """As below; with `known` (the host-known part of n_words, e.g. the window's draws) the words
+        come from the session's pool pipeline (_Pipeline): generated ahead on a side stream."""
+        dev = torch.device(device)
+        if known is not None and self._depth > 0 and self.device_generation and dev.type == "cuda" \
+                and self.pipeline_steps > 0:
+            self._close_pool()
+            mt = self._device_mt(dev)
+            p = self._pipe
+            if p is not None and (p.dev != dev or p.n < n_words):   # pools sized for smaller steps
+                self._leave_pipeline()
+                p = None
+            if p is None:
+                self._pipe = _Pipeline(dev, mt.state, int(n_words), int(known), self.pipeline_steps)
+            elif p.take(int(n_words)) is None:        # the pipeline lost its footing: start it again
+                self._leave_pipeline()
+                self._pipe = _Pipeline(dev, mt.state, int(n_words), int(known), self.pipeline_steps)
+            return
+        self._reserve_pool(n_words, device)
+
+    def _reserve_pool(self, n_words: int, device) -> None:
         """Inside a session: generate the words of SEVERAL calls in one go — an engine window's γ
         draws and its verify, whose word counts are known up front (2·B·V per draw, at most
         B·(γ + 2V) for the verify).  One set of jump-ahead substreams and one generation launch
@@ -179,6 +350,7 @@ class StreamNoise:
         dev = torch.device(device)
         if self._depth == 0 or not self.device_generation or dev.type != "cuda":
             return
+        self._leave_pipeline()
         self._close_pool()
         words = self._device_mt(dev).fill(int(n_words))
         self._pool = (words, 0)
@@ -192,9 +364,23 @@ class StreamNoise:
         if cursor or used_dev is not None:
             self._dev.commit(cursor, used_dev)
 
-    def prepare(self, n_words: int, device) -> torch.Tensor:
-        """Device words for a call that may consume up to n_words words."""
+    def prepare_ex(self, n_words: int, device):
+        """(words, host offset, device offset or None): the call's first word is
+        words[offset + *offset_dev] (sd_noise, ABI 11)."""
         dev = torch.device(device)
+        self._last_need = int(n_words)
+        if self._pipe is not None:
+            if self._pipe.dev == dev:
+                got = self._pipe.take(max(int(n_words), 1))
+                if got is not None:
+                    return got
+            self._leave_pipeline()
+        return self.prepare(n_words, device), 0, None
+
+    def prepare(self, n_words: int, device) -> torch.Tensor:
+        """Device words for a call that may consume up to n_words words (the words start at [0])."""
+        dev = torch.device(device)
+        self._leave_pipeline()   # a caller that needs the words at [0] (chunked windows)
         if not self.device_generation or dev.type != "cuda":
             return self.draw(n_words, dev)
         if self._pool is not None:
@@ -208,6 +394,9 @@ class StreamNoise:
         """The call consumed `count` words (or the device int64 `used_dev` holds the count)."""
         if self._dev is None:
             self.advance(int(used_dev.item()) if used_dev is not None else int(count or 0))
+            return
+        if self._pipe is not None:
+            self._pipe.consumed(count, used_dev, self._last_need)
             return
         if self._pool is not None:
             words, cursor = self._pool
@@ -231,6 +420,7 @@ class StreamNoise:
         finally:
             self._depth -= 1
             if self._depth == 0 and self._dev is not None:
+                self._leave_pipeline()
                 self._close_pool()
                 self._dev.pull(self.gen)
                 self._dev = None

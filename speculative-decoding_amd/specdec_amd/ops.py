@@ -193,8 +193,10 @@ def _noise_struct(noise, n_words_needed: int, device, row_base: int = 0):
     """(sd_noise, keepalive tensor) for a call that may consume up to n_words_needed words.
     row_base: global id of the call's row 0 (Philox noise is keyed by the global row)."""
     if isinstance(noise, StreamNoise):
-        words = noise.prepare(n_words_needed, device)
-        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, 0, 0, None), words
+        # the call's words start at words[offset + *offset_dev] (ABI 11; a pipelined session's pool)
+        words, off, off_dev = noise.prepare_ex(n_words_needed, device)
+        return _lib.sd_noise(_lib.SD_NOISE_STREAM, words.data_ptr(), words.numel(), 0, int(off), 0,
+                             off_dev.data_ptr() if off_dev is not None else None), (words, off_dev)
     if isinstance(noise, PhiloxNoise):
         if not 0 <= row_base < (1 << 24):
             raise ValueError("row_base must be in [0, 2^24)")

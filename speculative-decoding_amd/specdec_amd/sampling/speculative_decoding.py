@@ -158,7 +158,7 @@ def _speculative_generate(noise, inputs, drafter, target, gamma, logits_processo
             if k == 0 and isinstance(noise, StreamNoise) and spec.stochastic and row.device == torch.device(dev):
                 # the step's words in one generation: g draws of 2V, the verify's g + 2V
                 V = row.shape[-1]
-                noise.reserve(g * 2 * V + g + 2 * V, dev)
+                noise.reserve(g * 2 * V + g + 2 * V, dev, known=g * 2 * V)
             tok = ids_d[0, cur + k:cur + k + 1]
             sample_rows(row, kproc, noise, tokens_out=tok, row_stats_out=dstats[k] if stash else None, status_or=err_d)
             tok.clamp_(0, row.shape[-1] - 1)   # a failed row's -1 never reaches a forward
