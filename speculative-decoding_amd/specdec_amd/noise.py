@@ -101,6 +101,40 @@ class _Pool:
         self.dev_since = 0     # upper bound of the device-counted words since the anchor snapshot
 
 
+class _CudaBackend:
+    """The stream / event / generation primitives the pipeline runs on (a CPU test substitutes a
+    fake with the same methods: tests/test_stream_pipeline_cpu.py)."""
+
+    @staticmethod
+    def new_stream(dev):
+        return torch.cuda.Stream(dev)
+
+    @staticmethod
+    def current(dev):
+        return torch.cuda.current_stream(dev)
+
+    @staticmethod
+    def event_on(stream):
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        return ev
+
+    @staticmethod
+    def wait(stream, ev):
+        stream.wait_event(ev)
+
+    @staticmethod
+    def on(stream):
+        return torch.cuda.stream(stream)
+
+    @staticmethod
+    def keep(t, stream):
+        t.record_stream(stream)
+
+    generate = staticmethod(_mt_generate)
+    commit = staticmethod(_mt_commit)
+
+
 class _Pipeline:
     """STREAM words generated ahead, on a side stream, while the calls consume the current pool
     (DESIGN §4 "STREAM pool pipeline").  A session's steps (``reserve(n, known=...)``: n words at
@@ -108,24 +142,25 @@ class _Pipeline:
     start inside the current pool is host_off + *rel_dev (the kernels add both, ABI 11), rel_dev
     summing the verifies' device counts, so nothing is read back.  The next pool is generated from
     an anchor no later than where the current pool will be left: the position at the switch into
-    the current pool plus the host-known words of `steps` steps; it holds `steps` + 1 steps' worst
+    the current pool plus the host-known words of `steps` steps; it holds `steps` + 2 steps' worst
     case plus the verifies' slack, so the switch (after `steps` steps) always lands inside it and
     the pool after it is generated meanwhile, on the side stream, behind an event."""
 
-    def __init__(self, dev: torch.device, state: torch.Tensor, n: int, known: int, steps: int):
-        self.dev = dev
+    def __init__(self, dev: torch.device, state: torch.Tensor, n: int, known: int, steps: int, be=_CudaBackend):
+        self.dev, self.be = dev, be
         self.steps = steps
         self.n, self.known = n, known
-        self.cap = (steps + 1) * n + steps * (n - known)
-        self.side = torch.cuda.Stream(dev)
+        # a pool is entered up to one step's host words plus `steps` verifies' slack past its anchor,
+        # and serves `steps` steps (the switch is taken as soon as the walk passes the next anchor)
+        self.cap = (steps + 2) * n + steps * (n - known)
+        self.side = be.new_stream(dev)
         self.ws_main, self.ws_side = [None], [None]
         bufs = [torch.empty(self.cap + 624, dtype=torch.int32, device=dev) for _ in range(2)]
         self.pools = [_Pool(b, self.cap) for b in bufs]
         self.i = 0                                   # the current pool's buffer
         cur = self.pools[0]
         cur.state = state.clone()
-        main = torch.cuda.current_stream(dev)
-        _mt_generate(cur.state, cur.words, self.cap + 624, self.ws_main, main)   # the first pool: in line
+        be.generate(cur.state, cur.words, self.cap + 624, self.ws_main, be.current(dev))   # the first pool: in line
         self.host_off = 0
         self.rel_dev = torch.zeros(1, dtype=torch.long, device=dev)
         self.dev_hi = 0                              # upper bound of *rel_dev
@@ -139,22 +174,20 @@ class _Pipeline:
     def _enqueue_next(self) -> None:
         """Generate the other buffer's pool on the side stream, anchored at host_off + K + *rel_dev
         (snapshot) of the current pool, K = the host-known words of `steps` steps."""
-        main = torch.cuda.current_stream(self.dev)
+        be = self.be
         nxt = self.pools[1 - self.i]
         nxt.snap_host, nxt.K = self.host_off, self.steps * self.known
         nxt.a_dev = self.rel_dev.clone()             # snapshot (stream-ordered on the main stream)
         nxt.dev_since = 0
         nxt.state = self.cur.state.clone()
-        snap = torch.cuda.Event()
-        snap.record(main)                            # also orders the buffer's last readers before it
-        self.side.wait_event(snap)
-        with torch.cuda.stream(self.side):
-            nxt.a_dev.record_stream(self.side)
-            nxt.state.record_stream(self.side)
-            _mt_commit(nxt.state, self.cur.words, self.cap + 624, nxt.snap_host + nxt.K, nxt.a_dev, self.side)
-            _mt_generate(nxt.state, nxt.words, self.cap + 624, self.ws_side, self.side)
-            nxt.ready = torch.cuda.Event()
-            nxt.ready.record(self.side)
+        # the event also orders the buffer's last readers (the pool before the current one) first
+        be.wait(self.side, be.event_on(be.current(self.dev)))
+        with be.on(self.side):
+            be.keep(nxt.a_dev, self.side)
+            be.keep(nxt.state, self.side)
+            be.commit(nxt.state, self.cur.words, self.cap + 624, nxt.snap_host + nxt.K, nxt.a_dev, self.side)
+            be.generate(nxt.state, nxt.words, self.cap + 624, self.ws_side, self.side)
+            nxt.ready = be.event_on(self.side)
         self.nxt = nxt
 
     def fits(self, n: int) -> bool:
@@ -168,8 +201,7 @@ class _Pipeline:
         new_host = self.host_off - nxt.snap_host - nxt.K
         if new_host + nxt.dev_since + n > self.cap:
             return False
-        main = torch.cuda.current_stream(self.dev)
-        main.wait_event(nxt.ready)
+        self.be.wait(self.be.current(self.dev), nxt.ready)
         self.rel_dev.sub_(nxt.a_dev)                 # exact, on the device: >= 0, <= nxt.dev_since
         self.host_off, self.dev_hi = new_host, nxt.dev_since
         self.i = 1 - self.i
@@ -178,8 +210,10 @@ class _Pipeline:
         return True
 
     def take(self, n: int):
-        """(pool words, host offset, device offset) for a call of up to n words, or None."""
-        if not self.fits(n) and not self.switch(n):
+        """(pool words, host offset, device offset) for a call of up to n words, or None.  Moves to
+        the next pool as soon as the walk has passed its anchor (so every pool is entered within one
+        step of it), else stays while the call fits."""
+        if not self.switch(n) and not self.fits(n):
             return None
         return self.cur.words, self.host_off, self.rel_dev
 
@@ -195,8 +229,7 @@ class _Pipeline:
     def final_state(self) -> torch.Tensor:
         """The generator state after every consumed word (device; stream-ordered)."""
         st = self.cur.state.clone()
-        _mt_commit(st, self.cur.words, self.cap + 624, self.host_off, self.rel_dev,
-                   torch.cuda.current_stream(self.dev))
+        self.be.commit(st, self.cur.words, self.cap + 624, self.host_off, self.rel_dev, self.be.current(self.dev))
         return st
 
 
