@@ -598,11 +598,33 @@ __device__ __forceinline__ void stream_words(const sd_noise& nz, int64_t woff, i
     const int64_t w0 = woff + 2 * e0;
     const uint32_t* src = stream_ptr(nz) + w0;
     const int64_t cap = stream_cap(nz);
-    if (w0 + 2 * VEC <= cap && (reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+    const int s = (int)((reinterpret_cast<uintptr_t>(src) >> 2) & 3);   // words past a 16-byte boundary
+    if (s == 0 && w0 + 2 * VEC <= cap) {
 #pragma unroll
         for (int q = 0; q < VEC / 2; ++q) {
             const uint4 t = reinterpret_cast<const uint4*>(src)[q];
             w[4 * q] = t.x; w[4 * q + 1] = t.y; w[4 * q + 2] = t.z; w[4 * q + 3] = t.w;
+        }
+    } else if (s != 0 && w0 - s + 2 * VEC + 4 <= cap) {
+        // a call that starts mid-vector (a pipelined pool's offset is what the verifies consumed):
+        // one more aligned vector, and the words picked by a shift that is uniform per call (the
+        // row's offset sets it; e0 is a multiple of VEC), so per-word loads are never needed
+        uint32_t u[2 * VEC + 4];
+        const uint4* a = reinterpret_cast<const uint4*>(src - s);
+#pragma unroll
+        for (int q = 0; q <= VEC / 2; ++q) {
+            const uint4 t = a[q];
+            u[4 * q] = t.x; u[4 * q + 1] = t.y; u[4 * q + 2] = t.z; u[4 * q + 3] = t.w;
+        }
+        if (s == 1) {
+#pragma unroll
+            for (int k = 0; k < 2 * VEC; ++k) w[k] = u[k + 1];
+        } else if (s == 2) {
+#pragma unroll
+            for (int k = 0; k < 2 * VEC; ++k) w[k] = u[k + 2];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 2 * VEC; ++k) w[k] = u[k + 3];
         }
     } else {
 #pragma unroll

@@ -31,7 +31,12 @@ def test_cached_target_window_equals_uncached(mode):
     from types import SimpleNamespace
     from specdec_amd import set_noise_mode
     from specdec_amd.engine.infer_engine import batch_speculative_generate
-    target, drafter = tiny_llama(1, 2), tiny_llama(2, 1)
+    # the drafter: the target with a perturbed output layer, so drafts are accepted AND rejected (the
+    # rejected ones zeroed in place, whose cached keys / values the next window must recompute)
+    target, drafter = tiny_llama(1, 2), tiny_llama(1, 2)
+    with torch.no_grad():
+        g = torch.Generator(device=DEV).manual_seed(9)
+        drafter.lm_head.weight.add_(torch.randn(drafter.lm_head.weight.shape, generator=g, device=DEV) * 0.3)
     B, L = 4, 12
     ids = torch.randint(3, 4096, (B, L), generator=torch.Generator().manual_seed(4)).to(DEV)
     mask = torch.ones_like(ids)
@@ -46,4 +51,4 @@ def test_cached_target_window_equals_uncached(mode):
     set_noise_mode("stream")
     assert res[0][0] == res[1][0]
     assert res[0][1] == res[1][1]
-    assert any(r > 0 for r in res[0][1])   # some drafts were accepted: the cache crop was exercised
+    assert 0 < sum(res[0][1]) / len(res[0][1]) < 1   # accepts and rejects: the crop was exercised
