@@ -36,7 +36,18 @@ _DEVICE_GEN = os.environ.get("SPECDEC_STREAM_DEVICE", "1") != "0"
 # 41 M words at B = 32, V = 128256: 192 Ki words, 209 substreams).  SPECDEC_MT_STRIDE pins it.
 _STRIDE_ENV = os.environ.get("SPECDEC_MT_STRIDE")
 # steps per pipelined pool (StreamNoise.reserve(..., known=...) in a session); 0 = no pipeline
-_PIPE_STEPS = int(os.environ.get("SPECDEC_STREAM_PIPELINE", "4"))
+_PIPE_STEPS = int(os.environ.get("SPECDEC_STREAM_PIPELINE", "16"))
+# HBM the two pools may take (words): fewer steps per pool for big steps, no pipeline beyond it
+_PIPE_WORD_BUDGET = 1 << 30   # 4 GiB per pool
+
+
+def pipeline_steps_for(n: int, known: int, steps: int) -> int:
+    """Steps per pool for steps of n words (known host-known): the configured count, cut so a pool
+    (steps + 2 steps' worst case + the verifies' slack) fits the budget; 0 when even one step does not."""
+    w = n - known
+    while steps > 0 and (steps + 2) * n + steps * w > _PIPE_WORD_BUDGET:
+        steps -= 1
+    return steps
 MT_STRIDE = int(_STRIDE_ENV) if _STRIDE_ENV else 65536
 MT_MAX_SUBSTREAMS = 240
 
@@ -365,12 +376,15 @@ class StreamNoise:
             if p is not None and (p.dev != dev or p.n < n_words):   # pools sized for smaller steps
                 self._leave_pipeline()
                 p = None
-            if p is None:
-                self._pipe = _Pipeline(dev, mt.state, int(n_words), int(known), self.pipeline_steps)
-            elif p.take(int(n_words)) is None:        # the pipeline lost its footing: start it again
-                self._leave_pipeline()
-                self._pipe = _Pipeline(dev, mt.state, int(n_words), int(known), self.pipeline_steps)
-            return
+            steps = pipeline_steps_for(int(n_words), int(known), self.pipeline_steps)
+            if steps > 0:
+                if p is None:
+                    self._pipe = _Pipeline(dev, mt.state, int(n_words), int(known), steps)
+                elif p.take(int(n_words)) is None:        # the pipeline lost its footing: start it again
+                    self._leave_pipeline()
+                    self._pipe = _Pipeline(dev, mt.state, int(n_words), int(known), steps)
+                return
+            self._leave_pipeline()
         self._reserve_pool(n_words, device)
 
     def _reserve_pool(self, n_words: int, device) -> None:
