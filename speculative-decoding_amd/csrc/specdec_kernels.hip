@@ -157,10 +157,19 @@ struct Plan {
             if ((wg) >= 8192 && ((ph) == 1 || (ph) == 2)) P.ts[(size_t)(wg) * 16 + 14 + ((ph) == 2)] = __builtin_amdgcn_s_memtime(); \
         }                                                                                      \
     } while (0)
+// ticket mode: the work item a workgroup drew, one int64 per block id after the stamp table
+#define SD_TS_ROLE(wg, v)                                                                      \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && P.ts && (wg) < 32768) P.ts[(size_t)32768 * 16 + (wg)] = (v);   \
+    } while (0)
 #else
 #define SD_TS(wg, ph) \
     do {              \
         (void)(wg);   \
+    } while (0)
+#define SD_TS_ROLE(wg, v) \
+    do {                  \
+        (void)(wg);       \
     } while (0)
 #endif
 
@@ -518,6 +527,8 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
         decider = samp < 0 && item == n_span;
         s = slot_lo + (samp < 0 && item < n_span ? item / gx : 0);
         chunk = samp < 0 && item < n_span ? item % gx : 0;
+        SD_TS_ROLE(wg_id, ((int64_t)s_tk << 32) | ((int64_t)b << 12) |
+                              (samp >= 0 ? 0x800 | samp : (decider ? 0x400 : item)));
     } else if (SAMP && wg_id >= P.B * per_seq) {
         // the samplers come after every span and decider in dispatch order (block id): they only wait
         // for a decision, so the spans, which wait for nothing, always get their slots first, and a

@@ -60,8 +60,9 @@ def verify(target: Tensor, draft: Tensor, draft_tokens: Tensor, stop_tokens: Ten
     spec = _spec(kind, temperature, top_k, top_p) if rule == _lib.SD_RULE_SPEC else ops.PLAIN_SOFTMAX
     out = ops.verify([target[:, t] for t in range(target.shape[1])], [draft[:, d] for d in range(gamma)],
                      draft_tokens, rule, spec, spec, PhiloxNoise(seed, offset), stop_tokens, row_base=row_base)
-    return (out.n_accepted, out.next_token, out.resample_mass, out.prune_drafter, out.prune_target,
-            out.stop_index, out.row_status)
+    # ops.verify hands back views of one device buffer; a custom op's outputs may not alias each other
+    return tuple(t.clone() for t in (out.n_accepted, out.next_token, out.resample_mass, out.prune_drafter,
+                                     out.prune_target, out.stop_index, out.row_status))
 
 
 @verify.register_fake

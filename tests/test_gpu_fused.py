@@ -125,8 +125,15 @@ def test_fused_verify_polls_are_bounded():
         b = run(tl, dl, "engine", spec, 5)
         c = run(tl, dl, "engine", spec, 5)
     assert int(a["path"]) == _lib.SD_PATH_VERIFY_FUSED
-    assert (a["row_status"] & _lib.SD_ROW_EXCHANGE_TIMEOUT).all()
-    assert (a["row_status"] & _lib.SD_ROW_INVALID_DIST).all()
+    # a row whose records were all in at its first read never waits, so it completes normally even
+    # with every wait forbidden: each row is either flagged (timeout + invalid) or the clean call's row
+    flagged = (a["row_status"] & _lib.SD_ROW_EXCHANGE_TIMEOUT) != 0
+    assert flagged.any(), a["row_status"]
+    assert (a["row_status"][flagged] & _lib.SD_ROW_INVALID_DIST).all()
+    clean = ~flagged
+    assert not (a["row_status"][clean] & _lib.SD_ROW_ERROR_MASK).any()
+    for k in ("n_accepted", "next_token", "row_status"):
+        assert torch.equal(a[k][clean], ref[k][clean]), k
     for o in (b, c):
         assert int(o["path"]) == _lib.SD_PATH_VERIFY_FUSED
         assert not (o["row_status"] & (_lib.SD_ROW_EXCHANGE_TIMEOUT | _lib.SD_ROW_INVALID_DIST)).any()
