@@ -298,6 +298,9 @@ typedef enum {
                                    that many 2048-element stages per workgroup                    */
     SD_OPT_TICKET_LAG = 7,      /* ABI 11. 0 (default, 2): in the ticket-order fused verify, how many
                                    sequences of a label stream before an earlier one's samplers  */
+    SD_OPT_SAMP_CHUNKS = 8,     /* ABI 11. 0 (default: 2, 4 in ticket order): 2048-element chunks each
+                                   sampling workgroup of the fused verify draws; 2, 4 or 8 pin it
+                                   (the same chunks and draws whatever the grouping)              */
 } sd_option;
 int32_t sd_set_option(int32_t option, int32_t value);
 int32_t sd_get_option(int32_t option, int32_t* value);

@@ -58,8 +58,9 @@ for rep in range(3):
     role = raw[NWG * 16:]
     live = t[:, 0] > 0
     t0 = t[live, 0].min()
-    d = (t - t0) / 100.0
-    d[t == 0] = np.nan
+    # columns 12-15 of workgroups past 8192 hold s_memtime (shader clock) stamps: not times here
+    d = (t[:, :12] - t0) / 100.0
+    d[t[:, :12] == 0] = np.nan
     r = role & 0xfff
     kind = np.where(~live, -1, np.where(r & 0x800, 2, np.where(r & 0x400, 1, 0)))   # 0 span 1 decider 2 sampler
     end = np.nanmax(d, axis=1)
@@ -95,6 +96,7 @@ for rep in range(3):
     dw = np.nansum(d[dec, 9] - d[dec, 0]) + np.nansum(end[dec] - d[dec, 3])
     print(f"  of which waiting: samplers {sw / tot * 100:.1f} %, deciders {dw / tot * 100:.1f} %")
     # concurrency in 5 us bins: workgroups alive per role
+    assert make < 1e5, make   # a stamp outside this launch: do not build a giant bin table
     bins = np.arange(0, make + 5, 5.0)
     rows = []
     for lo in bins[:-1]:

@@ -115,6 +115,7 @@ struct Plan {
     uint4* drec;          // fused verify: per sequence two tagged decision records for its samplers
     uint4* crec;          // fused verify, split records: the chunks' candidates, apart from their totals
     int32_t n_samp;       // fused verify (k_stats<.., SAMP>): sampling workgroups per sequence
+    int32_t samp_cps;     //   chunks (of rchunk elements) each sampling workgroup draws: 2, 4 or 8
     int32_t ticket;       // fused verify, any batch: work items by arrival ticket (fused_role), not block id
     int32_t lag;          //   ticket mode: a sequence's samplers come after the spans of the label's lag-th next
     int32_t labels;       //   ticket mode: label = block id % labels, one ticket counter and one sequence set each
@@ -764,8 +765,16 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
 
 // The fused verify (stats_body with SAMP): grid = B x (spans + decider) then B x n_samp samplers (two
 // 2048-element chunks each)
+#ifndef SD_FUSED_VGPR
+#define SD_FUSED_VGPR 0
+#endif
+#if SD_FUSED_VGPR > 0
+#define SD_FUSED_VGPR_CAP __attribute__((amdgpu_waves_per_eu(SD_FUSED_VGPR)))
+#else
+#define SD_FUSED_VGPR_CAP
+#endif
 template <int DT, bool FAST>
-__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_verify_fused(Plan P, int slot_lo, int slot_cnt) {
+__global__ void __launch_bounds__(kThreads) SD_SGPR_CAP SD_FUSED_VGPR_CAP k_verify_fused(Plan P, int slot_lo, int slot_cnt) {
     stats_body<DT, FAST, true, true>(P, slot_lo, slot_cnt);
 }
 
@@ -1348,9 +1357,12 @@ __device__ __forceinline__ void decide_seq(const Plan& P, int b, const DraftPf& 
                         __builtin_amdgcn_s_sleep(1);
                         rr = ld_coh16(rp[k]);
                     }
-                    v[k] = rr.z == tag ? make_float2(__uint_as_float(rr.x), __uint_as_float(rr.y))
-                                       : make_float2(0.f, NAN);   // timeout: the row is flagged invalid
-                    lost |= rr.z != tag;
+                    // spin limit < 0 (the test hook): every record counts as lost, as in the draws'
+                    // and the samplers' polls — not only the ones still missing at the first read
+                    const bool got = rr.z == tag && P.spin_limit >= 0;
+                    v[k] = got ? make_float2(__uint_as_float(rr.x), __uint_as_float(rr.y))
+                               : make_float2(0.f, NAN);   // timeout: the row is flagged invalid
+                    lost |= !got;
                 }
             }
             SD_TS(wg_id, 11);
@@ -2334,6 +2346,7 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
 #define SD_SAMP_SLEEP 1   // fused samplers' decision poll interval (s_sleep units of 64 clocks)
 #endif
 constexpr int kFusedEpt = 8;                       // k_sample's chunking: 2048-element chunks, the same draws
+constexpr int kMaxSampPairs = 4;                   // chunk pairs per sampler: samp_cps <= 8
 
 __device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
     uint32_t h = epoch * 0x9E3779B1u + (uint32_t)b * 0x85EBCA77u + (uint32_t)k * 0xC2B2AE3Du + 0x1B873593u;
@@ -2419,10 +2432,14 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     __shared__ uint32_t s_ep;
     __shared__ int32_t s_ok;
     SD_TS(wg_id, 0);
-    // the two chunks' in-chunk uniforms depend on (b, c) only: computed (and the Philox offset, a
-    // device load under graph replays, fetched) while the decision is still being made
-    const double u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)c));
-    const double u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)c));
+    // sampler c draws chunks [c * cps, c * cps + cps) of the sequence's rn_chunks, in pairs (pair q:
+    // chunks 2q, 2q + 1 of the row); the chunks, their uniforms and their records are k_sample's,
+    // so the grouping never changes a draw
+    const int cps = P.samp_cps, q0 = c * (cps >> 1), nq = cps >> 1;
+    // the first pair's in-chunk uniforms depend on (b, chunk) only: computed (and the Philox offset,
+    // a device load under graph replays, fetched) while the decision is still being made
+    double u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)q0));
+    double u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)q0));
     if (threadIdx.x < kWave) {
         const int lane = threadIdx.x;
         uint32_t ep = 0;
@@ -2459,45 +2476,66 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     // (SD_ROW_EXCHANGE_TIMEOUT) without it.
     if (!ok) return;
     if (d.mode <= kModeNone || d.mode > kModePRow || d.slot < 0 || d.slot >= P.n_tslots) {
-        // nothing to draw: empty records for both chunks (the decider waits for every sampler)
-        if (threadIdx.x < 2 && 2 * c + (int)threadIdx.x < P.rn_chunks) {
-            const int cc = 2 * c + (int)threadIdx.x;
+        // nothing to draw: empty records for every chunk of this sampler (the decider waits for all)
+        if ((int)threadIdx.x < cps && 2 * q0 + (int)threadIdx.x < P.rn_chunks) {
+            const int cc = 2 * q0 + (int)threadIdx.x;
             st_coh16(reinterpret_cast<float4*>(P.sprec) + (int64_t)b * P.rn_chunks + cc,
                      make_uint4(0u, 0u, (uint32_t)-1, sample_tag(ep, b, cc)));
         }
         return;
     }
     const PairRows R = pair_rows<DT, DT>(P, d, b);
-    // chunks 2c and 2c + 1 of the decided rows: every vector of both in flight at once, then each
-    // chunk's weights and draw (k_sample's chunking and uniforms: the same draws)
     constexpr int VEC = Elem<DT>::kVec, NV = kFusedEpt / VEC;
-    const int c0 = 2 * c, c1 = 2 * c + 1;
-    const bool has1 = c1 < P.rn_chunks;
     if (!(R.t_al && (!R.resid || R.d_al) && P.V >= VEC)) {   // misaligned rows: one chunk at a time
-        sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c0, sample_tag(ep, b, c0), wg_id, u0);
-        if (has1) sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c1, sample_tag(ep, b, c1), wg_id, u1);
+#pragma unroll
+        for (int k = 0; k < kMaxSampPairs; ++k) {
+            const int q = q0 + k, c0 = 2 * q, c1 = 2 * q + 1;
+            if (k >= nq || c0 >= P.rn_chunks) break;
+            if (k > 0) {
+                u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)q));
+                u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)q));
+            }
+            sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c0, sample_tag(ep, b, c0), wg_id, u0);
+            if (c1 < P.rn_chunks) sample_chunk<DT, DT, FAST, kFusedEpt>(P, R, b, c1, sample_tag(ep, b, c1), wg_id, u1);
+        }
         return;
     }
     const int64_t lastv = last_whole_vec<DT>(P.V);
     float wv[kFusedEpt], psum;
     if constexpr (NV == 1 && FAST) {
-        // 16-bit rows (one vector per thread and chunk): both chunks' vectors in flight at once, then
-        // each chunk's weights (the sampled row's mode and the chunk's raggedness hoisted out of the
-        // element loop) and draw
-        const int64_t e0 = (int64_t)c0 * P.rchunk + (int64_t)threadIdx.x * VEC, e1 = e0 + P.rchunk;
-        const uint4 t0 = ld16_clamped<DT>(R.trow, e0, lastv);
-        const uint4 d0 = R.resid ? ld16_clamped<DT>(R.drow, e0, lastv) : make_uint4(0u, 0u, 0u, 0u);
-        uint4 t1 = make_uint4(0u, 0u, 0u, 0u), d1 = t1;
-        if (has1) {
-            t1 = ld16_clamped<DT>(R.trow, e1, lastv);
-            if (R.resid) d1 = ld16_clamped<DT>(R.drow, e1, lastv);
-        }
-        fused_weights<DT>(R, c0, P.rchunk, e0, t0, d0, wv, psum);
-        SD_TS(wg_id, 8);
-        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id, u0);
-        if (has1) {
-            fused_weights<DT>(R, c1, P.rchunk, e1, t1, d1, wv, psum);
-            sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
+        // 16-bit rows (one vector per thread and chunk): a pair's four vectors in flight at once, the
+        // next pair's issued before this pair's weights and draws (the sampled row's mode and the
+        // chunk's raggedness hoisted out of the element loop)
+        const int64_t tid8 = (int64_t)threadIdx.x * VEC;
+        auto ld_pair = [&](int q, uint4& t0, uint4& d0, uint4& t1, uint4& d1) {
+            const int64_t e0 = (int64_t)(2 * q) * P.rchunk + tid8, e1 = e0 + P.rchunk;
+            t0 = ld16_clamped<DT>(R.trow, e0, lastv);
+            d0 = R.resid ? ld16_clamped<DT>(R.drow, e0, lastv) : make_uint4(0u, 0u, 0u, 0u);
+            t1 = make_uint4(0u, 0u, 0u, 0u);
+            d1 = t1;
+            if (2 * q + 1 < P.rn_chunks) {
+                t1 = ld16_clamped<DT>(R.trow, e1, lastv);
+                if (R.resid) d1 = ld16_clamped<DT>(R.drow, e1, lastv);
+            }
+        };
+#pragma unroll
+        for (int k = 0; k < kMaxSampPairs; ++k) {
+            const int q = q0 + k, c0 = 2 * q, c1 = 2 * q + 1;
+            if (k >= nq || c0 >= P.rn_chunks) break;
+            uint4 t0, d0, t1, d1;
+            ld_pair(q, t0, d0, t1, d1);
+            if (k > 0) {
+                u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)q));
+                u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)q));
+            }
+            const int64_t e0 = (int64_t)c0 * P.rchunk + tid8, e1 = e0 + P.rchunk;
+            fused_weights<DT>(R, c0, P.rchunk, e0, t0, d0, wv, psum);
+            SD_TS(wg_id, 8);
+            sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id, u0);
+            if (c1 < P.rn_chunks) {
+                fused_weights<DT>(R, c1, P.rchunk, e1, t1, d1, wv, psum);
+                sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
+            }
         }
         SD_TS(wg_id, 2);
         return;
@@ -2526,15 +2564,25 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     };
     // the general rows (fp32, processors): chunk c0's vectors, its weights, then chunk c1's loads go
     // out before c0's draw; only the weights of one chunk and the raw vectors of the other are live
-    issue(c0);
-    weights(c0, wv, psum);
-    if (NV == 1 && has1) issue(c1);   // fp32 rows (two vectors per chunk): after the draw, no spills
-    SD_TS(wg_id, 8);
-    sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id, u0);
-    if (has1) {
-        if (NV != 1) issue(c1);
-        weights(c1, wv, psum);
-        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
+#pragma unroll
+    for (int k = 0; k < kMaxSampPairs; ++k) {
+        const int q = q0 + k, c0 = 2 * q, c1 = 2 * q + 1;
+        if (k >= nq || c0 >= P.rn_chunks) break;
+        const bool has1 = c1 < P.rn_chunks;
+        if (k > 0) {
+            u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)q));
+            u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)q));
+        }
+        issue(c0);
+        weights(c0, wv, psum);
+        if (NV == 1 && has1) issue(c1);   // fp32 rows (two vectors per chunk): after the draw, no spills
+        SD_TS(wg_id, 8);
+        sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c0, wv, psum, sample_tag(ep, b, c0), wg_id, u0);
+        if (has1) {
+            if (NV != 1) issue(c1);
+            weights(c1, wv, psum);
+            sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
+        }
     }
     SD_TS(wg_id, 2);
 }
@@ -3019,6 +3067,37 @@ __device__ int greedy_rescan(const DrawLean& A, const char* row, int c, float M,
     return bi;
 }
 
+// Element k of a lane's NST packed 16-byte vectors (16-bit rows): the loaded bits stay packed in
+// registers and every pass over the span unpacks them again (one shift or mask for bf16), so a
+// 4-stage span holds 16 VGPRs of row data instead of 32 floats plus 32 weights (90 -> <= 64 VGPRs:
+// 8 workgroups per CU instead of 5, the large-batch draws' bytes in flight).
+template <int DT>
+__device__ __forceinline__ float lean_elem(const uint4* raw, int k) {
+    const uint4 q = raw[k >> 3];
+    const int i = (k & 7) >> 1;
+    const uint32_t wd = i == 0 ? q.x : (i == 1 ? q.y : (i == 2 ? q.z : q.w));
+    if constexpr (DT == SD_BF16) return __uint_as_float((k & 1) ? (wd & 0xffff0000u) : (wd << 16));
+    else return __half2float(__ushort_as_half((unsigned short)((k & 1) ? (wd >> 16) : (wd & 0xffffu))));
+}
+
+// The ragged last span's vector at e0 in packed form: elements at or past the row end become -inf
+// (bf16 0xff80, fp16 0xfc00), and a vector the clamped load could not fetch whole is rebuilt from
+// guarded 16-bit loads — the same values finish16 + the -inf mask gave as floats.
+template <int DT>
+__device__ __forceinline__ uint4 lean_finish16(uint4 w, const char* row, int64_t e0, int vocab) {
+    if (e0 + 8 <= vocab) return w;
+    constexpr uint32_t kNegInf = DT == SD_BF16 ? 0xff80u : 0xfc00u;
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(row);
+    uint32_t ws[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int64_t e = e0 + 2 * k;
+        const uint32_t lo = e < vocab ? (uint32_t)h[e] : kNegInf, hi = e + 1 < vocab ? (uint32_t)h[e + 1] : kNegInf;
+        ws[k] = lo | (hi << 16);
+    }
+    return make_uint4(ws[0], ws[1], ws[2], ws[3]);
+}
+
 template <int DT, int NST, bool GREEDY = false>
 __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     constexpr int VEC = 8, STEP = kThreads * VEC, EPT = NST * VEC, NW = kThreads / kWave;
@@ -3029,27 +3108,28 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     SD_TSL(ts_wg, 0);
     const char* row = A.rows + (int64_t)r * A.stride_bytes;
     const int64_t base = (int64_t)c * NST * STEP;
-    float y[EPT];
+    uint4 raw[NST];
     if (base + (int64_t)NST * STEP <= A.V) {
-        uint4 raw[NST];
 #pragma unroll
         for (int v = 0; v < NST; ++v)
             raw[v] = *reinterpret_cast<const uint4*>(row + (base + (int64_t)v * STEP + threadIdx.x * VEC) * 2);
-#pragma unroll
-        for (int v = 0; v < NST; ++v) unpack16<DT>(raw[v], y + v * VEC);
     } else {   // the row's ragged last span
         const int64_t last = last_whole_vec<DT>(A.V);
-        uint4 raw[NST];
 #pragma unroll
         for (int v = 0; v < NST; ++v) raw[v] = ld16_clamped<DT>(row, base + (int64_t)v * STEP + threadIdx.x * VEC, last);
 #pragma unroll
-        for (int v = 0; v < NST; ++v) {
-            const int64_t e0 = base + (int64_t)v * STEP + threadIdx.x * VEC;
-            finish16<DT>(raw[v], row, e0, A.V, y + v * VEC);
-#pragma unroll
-            for (int k = 0; k < VEC; ++k) y[v * VEC + k] = e0 + k < A.V ? y[v * VEC + k] : -INFINITY;
-        }
+        for (int v = 0; v < NST; ++v)
+            raw[v] = lean_finish16<DT>(raw[v], row, base + (int64_t)v * STEP + threadIdx.x * VEC, A.V);
     }
+    auto y = [&](int k) { return lean_elem<DT>(raw, k); };
+    // an empty asm that "rewrites" the packed vectors: the passes after it cannot reuse values the
+    // compiler derived from them before (it would keep every unpacked element and weight live)
+    // (one stage already fits 64 VGPRs: the bench shape's draw keeps the compiler's schedule)
+    auto fence_raw = [&]() {
+        if constexpr (NST > 1)
+#pragma unroll
+        for (int v = 0; v < NST; ++v) asm volatile("" : "+v"(raw[v].x), "+v"(raw[v].y), "+v"(raw[v].z), "+v"(raw[v].w));
+    };
     __shared__ float l_m[NW], l_s[NW];
     __shared__ double l_u;
     __shared__ int32_t l_j;
@@ -3062,22 +3142,23 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         if (lane == 0) { l_u = u; l_j = -1; l_y = -INFINITY; }
     }
     // per-wave max and weights: no barrier before the exps
-    float mv = y[0];
+    float mv = y(0);
 #pragma unroll
-    for (int k = 1; k < EPT; ++k) mv = fmaxf(mv, y[k]);
+    for (int k = 1; k < EPT; ++k) mv = fmaxf(mv, y(k));
     // integer-key wave max; a wave of -inf entries subtracts 0 (its weights are exp2(-inf) = 0),
     // so no per-element select, and a NaN entry always makes its own weight NaN (the span's S_c
     // NaN flags the row)
+    fence_raw();
     const float mw = wave_max_ord(mv);
     const float mws = mw > -INFINITY ? mw : 0.f;
     SD_TSL(ts_wg, 1);
-    float wv[EPT];
+    // element k's weight, recomputed where it is needed again (the claiming lane's walk): the same
+    // instruction on the same input, so the walk sees exactly the summed values
+    auto wv = [&](int k) { return __builtin_amdgcn_exp2f((y(k) - mws) * kLog2e); };
     float tl = 0.f;
 #pragma unroll
-    for (int k = 0; k < EPT; ++k) {
-        wv[k] = __builtin_amdgcn_exp2f((y[k] - mws) * kLog2e);
-        tl += wv[k];
-    }
+    for (int k = 0; k < EPT; ++k) tl += wv(k);
+    fence_raw();
     const float incl = wave_incl_scan(tl);             // lane order, relative to mw
     const float prev = dpp_f<0x138, 0xF, true>(0.f, incl);   // wave_shr:1 -> the previous lane's incl
     if (lane == 63) { l_m[w] = mw; l_s[w] = incl; }
@@ -3105,8 +3186,8 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
         for (int k = 0; k < EPT; ++k) {
             const int v = k / VEC;
             const int32_t j = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + (k - v * VEC));
-            if (y[k] == m && fi == INT_MAX) fi = j;
-            dirty |= y[k] > m - kGreedyDelta && y[k] != m;
+            if (y(k) == m && fi == INT_MAX) fi = j;
+            dirty |= y(k) > m - kGreedyDelta && y(k) != m;
         }
         fi = wave_min_i(fi);
         const bool dw = __ballot(dirty) != 0;
@@ -3128,8 +3209,9 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             int kk = -1, lastk = -1;
 #pragma unroll
             for (int k = 0; k < EPT; ++k) {
-                run = fmaf(wv[k], my_sc, run);
-                if (wv[k] > 0.f) {
+                const float wk = wv(k);
+                run = fmaf(wk, my_sc, run);
+                if (wk > 0.f) {
                     lastk = k;
                     if (kk < 0 && run > t) kk = k;
                 }
@@ -3137,9 +3219,9 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
             if (kk < 0) kk = lastk;
             if (kk >= 0) {
                 const int v = kk / VEC;
-                float yk = y[0];
+                float yk = y(0);
 #pragma unroll
-                for (int k = 1; k < EPT; ++k) yk = k == kk ? y[k] : yk;
+                for (int k = 1; k < EPT; ++k) yk = k == kk ? y(k) : yk;
                 cj = (int32_t)(base + ((int64_t)v * kThreads + threadIdx.x) * VEC + (kk - v * VEC));
                 cy = yk;
             }
@@ -3430,12 +3512,13 @@ void policy_init() {
 
 // Dispatch options (sd_set_option), indexed by sd_option; relaxed reads on every call.
 std::atomic<int> g_opt_fused{1}, g_opt_lean{-1}, g_opt_thr_poll{1}, g_opt_draw_stream{1}, g_opt_ticket{-1};
-std::atomic<int> g_opt_draw_span{0}, g_opt_ticket_lag{0};
+std::atomic<int> g_opt_draw_span{0}, g_opt_ticket_lag{0}, g_opt_samp_chunks{0};
 constexpr int kDrawSpan2MinB = 64, kDrawSpan4MinB = 256;   // k_draw_lean: batches above take 2 / 4 stages
 std::atomic<int>* option_slot(int32_t opt) {
     switch (opt) {
         case SD_OPT_DRAW_SPAN: return &g_opt_draw_span;
         case SD_OPT_TICKET_LAG: return &g_opt_ticket_lag;
+        case SD_OPT_SAMP_CHUNKS: return &g_opt_samp_chunks;
         case SD_OPT_FUSED_VERIFY: return &g_opt_fused;
         case SD_OPT_FUSED_TICKET: return &g_opt_ticket;
         case SD_OPT_LEAN_VERIFY: return &g_opt_lean;
@@ -3504,6 +3587,7 @@ void carve(Plan& P, Carve& c, int rows_total, int B, int gamma, int vocab) {
     P.drec = nullptr;
     P.crec = nullptr;
     P.n_samp = 0;
+    P.samp_cps = 2;
     P.keep_hist = c.take<int32_t>((size_t)rows_total * kThreshScratchInts);
     P.thr_part = c.take<uint32_t>((size_t)rows_total * kThrMaxSlices);
     P.thr_tail = c.take<float>((size_t)rows_total * kThrMaxSlices);
@@ -3637,6 +3721,7 @@ int32_t launch_fused(const sd::Plan& P, void* stream) {
 constexpr int kTicketMinB = 64;
 constexpr int kTicketLabels = 64;   // labels (ticket counters) from B = 64; 8 below
 constexpr int kTicketLag = 2;       // default lag (SD_OPT_TICKET_LAG pins it)
+constexpr int kTicketSampChunks = 4;   // chunks per sampler in ticket order (SD_OPT_SAMP_CHUNKS pins it): 4 measured best at B = 128 / 512
 constexpr int kTicketSpan = 16 * kThreads * 8;   // 32768 elements: 4 spans per Llama-3 row
 bool fused_layout(sd::Plan& F) {
     const int cap = resident_cap(fused_kernel(F));
@@ -3646,15 +3731,18 @@ bool fused_layout(sd::Plan& F) {
     F.ticket = tmode == 1 || (tmode < 0 && (F.B >= kTicketMinB || !resident));
     if (!F.ticket) return resident;
     if (cap <= 0) return false;
-    const int per_unit = F.n_tslots * F.n_chunks + 1 + F.n_samp;
     F.labels = F.B >= kTicketLabels ? kTicketLabels : 8;
+    // chunks per sampler: a large batch's samplers hold slots the spans could stream in, and each
+    // one pays a decision poll and a dispatch — fewer, longer samplers (SD_OPT_SAMP_CHUNKS pins it)
+    const int sc = opt(g_opt_samp_chunks);
+    F.samp_cps = sc > 0 ? sc : kTicketSampChunks;
+    F.n_samp = (F.rn_chunks + F.samp_cps - 1) / F.samp_cps;
     const int lg = opt(g_opt_ticket_lag);
     F.lag = lg > 0 ? lg : kTicketLag;
     // set 1's last `labels` counters (k_sample's arrivals of sequences B >= kCntMax - labels, which a
     // call of that size only uses in counter mode, where they are zero between launches too)
     F.ticket_ctr = F.cnt + ((size_t)1 * kCntMax + (kCntMax - F.labels)) * kCntStride;
     F.xcd_affine = 0;
-    (void)per_unit;
     return true;
 }
 
@@ -4027,6 +4115,7 @@ int32_t sd_set_option(int32_t option, int32_t value) {
                   : option == SD_OPT_LEAN_VERIFY || option == SD_OPT_FUSED_TICKET ? (value >= -1 && value <= 1)
                   : option == SD_OPT_DRAW_SPAN ? (value == 0 || value == 1 || value == 2 || value == 4)
                   : option == SD_OPT_TICKET_LAG ? (value >= 0 && value <= 64)
+                  : option == SD_OPT_SAMP_CHUNKS ? (value == 0 || value == 2 || value == 4 || value == 8)
                                                  : (value == 0 || value == 1);
     if (!ok) return SD_ERR_INVALID;
     o->store(value, std::memory_order_relaxed);
@@ -4167,7 +4256,8 @@ int32_t sd_verify(const sd_verify_args* a, void* stream) {
             Plan F = P;
             F.rchunk = kThreads * kFusedEpt;
             F.rn_chunks = (P.V + F.rchunk - 1) / F.rchunk;
-            F.n_samp = (F.rn_chunks + 1) / 2;   // two chunks per sampler (fused_sampler)
+            F.samp_cps = 2;                     // two chunks per sampler (fused_sampler); ticket order: below
+            F.n_samp = (F.rn_chunks + 1) / 2;
             const bool layout_ok = fused_layout(F);   // block-id or ticket order; may re-cut the spans
             // records: the spans' (srec = rpart), the samplers' totals after them, the decisions, the candidates
             const size_t n_srec = (size_t)P.B * P.stat_slots * F.n_chunks;

@@ -34,7 +34,7 @@ SD_ROW_ERROR_MASK = SD_ROW_INVALID_DIST | SD_ROW_NOISE_OVERRUN | SD_ROW_EXCHANGE
 
 # dispatch options (sd_set_option) and the paths sd_last_*_path reports
 SD_OPT_FUSED_VERIFY, SD_OPT_LEAN_VERIFY, SD_OPT_THRESHOLD_POLL, SD_OPT_DRAW_STREAM = 1, 2, 3, 4
-SD_OPT_FUSED_TICKET, SD_OPT_DRAW_SPAN, SD_OPT_TICKET_LAG = 5, 6, 7
+SD_OPT_FUSED_TICKET, SD_OPT_DRAW_SPAN, SD_OPT_TICKET_LAG, SD_OPT_SAMP_CHUNKS = 5, 6, 7, 8
 SD_PATH_NONE = 0
 SD_PATH_VERIFY_LEAN, SD_PATH_VERIFY_FUSED, SD_PATH_VERIFY_TWO_LAUNCH, SD_PATH_VERIFY_STREAM = 1, 2, 3, 4
 SD_PATH_VERIFY_FUSED_TICKET = 5

@@ -105,7 +105,9 @@ def test_draw_distribution(sd, label, proc, V, dtype):
 
 @pytest.mark.parametrize("R,V,dtype,offset", [(32, 128256, torch.bfloat16, 0), (5, 50257, torch.float32, 0),
                                               (3, 1000, torch.bfloat16, 0), (4, 4099, torch.bfloat16, 1),
-                                              (8, 50257, torch.float16, 0)])
+                                              (8, 50257, torch.float16, 0),
+                                              # k_draw_lean's 2- and 4-stage spans (large batches)
+                                              (100, 128256, torch.bfloat16, 0), (300, 128256, torch.bfloat16, 0)])
 def test_draw_row_stats_reproduce_softmax(sd, R, V, dtype, offset):
     """(M, S) from the draw: exp(y - M) / S is the softmax of the row (fp64 oracle) to 2e-6
     relative on the largest probabilities; misaligned rows (offset 1) and ragged V included."""

@@ -72,19 +72,28 @@ def ticket(value):
     return _lib.option(_lib.SD_OPT_FUSED_TICKET, value)
 
 
-@pytest.mark.parametrize("B,V,tk", [(8, 128256, -1), (32, 128256, -1), (16, 50257, -1),
-                                    # ticket order: forced at small batches, by default from B = 64
-                                    (8, 128256, 1), (32, 128256, 1), (128, 128256, -1), (300, 50257, -1)])
+def samp_chunks(value):
+    from specdec_amd import _lib
+    return _lib.option(_lib.SD_OPT_SAMP_CHUNKS, value)
+
+
+@pytest.mark.parametrize("B,V,tk,sc", [(8, 128256, -1, 0), (32, 128256, -1, 0), (16, 50257, -1, 0),
+                                       # ticket order: forced at small batches, by default from B = 64
+                                       (8, 128256, 1, 0), (32, 128256, 1, 0), (128, 128256, -1, 0),
+                                       (300, 50257, -1, 0),
+                                       # chunks per sampler (ticket order; 4 by default there)
+                                       (128, 128256, -1, 2), (128, 128256, -1, 8), (300, 50257, -1, 2),
+                                       (8, 128256, 1, 4)])
 @pytest.mark.parametrize("rule", ["engine", "spec"])
 @pytest.mark.parametrize("proc", PROCS, ids=[f"{p[0]}-T{p[1]}" for p in PROCS])
-def test_fused_verify_equals_two_launch_verify(B, V, tk, rule, proc):
+def test_fused_verify_equals_two_launch_verify(B, V, tk, sc, rule, proc):
     from specdec_amd import ops
     spec = ops.ProcSpec(*proc)
     seed = 31 * B + V % 89 + (1 if rule == "spec" else 2)
     tl, dl = inputs(B, 4, V, rule, seed)
     engine = rule == "engine"
     from specdec_amd import _lib
-    with fused(1), ticket(tk):
+    with fused(1), ticket(tk), samp_chunks(sc):
         a = run(tl, dl, rule, spec, seed, engine)
     with fused(0):
         b = run(tl, dl, rule, spec, seed, engine)
@@ -117,23 +126,21 @@ def test_fused_verify_polls_are_bounded():
         finally:
             set_poll_policy(*old)
 
+    with fused(0):   # the two-launch path: an independent reference for every row
+        two = run(tl, dl, "engine", spec, 5)
     with fused(1):
         ref = run(tl, dl, "engine", spec, 5)
+        for k in ("n_accepted", "next_token", "row_status"):
+            assert torch.equal(ref[k], two[k]), (k, (ref[k] != two[k]).nonzero().flatten(), ref["row_status"])
         a = run(tl, dl, "engine", spec, 5, verify_ctx=no_polls)
         # the next calls on the same workspace are healthy: nothing the timed-out call left behind (its
         # records, its samplers, its epoch) is taken as theirs — no flags, the same outputs as before
         b = run(tl, dl, "engine", spec, 5)
         c = run(tl, dl, "engine", spec, 5)
     assert int(a["path"]) == _lib.SD_PATH_VERIFY_FUSED
-    # a row whose records were all in at its first read never waits, so it completes normally even
-    # with every wait forbidden: each row is either flagged (timeout + invalid) or the clean call's row
-    flagged = (a["row_status"] & _lib.SD_ROW_EXCHANGE_TIMEOUT) != 0
-    assert flagged.any(), a["row_status"]
-    assert (a["row_status"][flagged] & _lib.SD_ROW_INVALID_DIST).all()
-    clean = ~flagged
-    assert not (a["row_status"][clean] & _lib.SD_ROW_ERROR_MASK).any()
-    for k in ("n_accepted", "next_token", "row_status"):
-        assert torch.equal(a[k][clean], ref[k][clean]), k
+    # every row flagged: the hook makes every poll give up, the decider's span records included
+    assert (a["row_status"] & _lib.SD_ROW_EXCHANGE_TIMEOUT).all(), a["row_status"]
+    assert (a["row_status"] & _lib.SD_ROW_INVALID_DIST).all()
     for o in (b, c):
         assert int(o["path"]) == _lib.SD_PATH_VERIFY_FUSED
         assert not (o["row_status"] & (_lib.SD_ROW_EXCHANGE_TIMEOUT | _lib.SD_ROW_INVALID_DIST)).any()
