@@ -326,6 +326,10 @@ __device__ __forceinline__ void block_argmax(float& v, int32_t& i, float* ldsv, 
 #define SD_STATS_PIPE 4
 #endif
 constexpr int kPipe = SD_STATS_PIPE;
+#ifndef SD_TICKET_PIPE
+#define SD_TICKET_PIPE 4
+#endif
+constexpr int kTicketPipe = SD_TICKET_PIPE;   // the ticket-order fused verify's spans
 constexpr float kLog2e = 1.44269502162933349609375f;
 
 __device__ __forceinline__ void online_merge(float& m, float& s, float m2, float s2) {
@@ -459,7 +463,11 @@ __device__ __forceinline__ void fused_role(int t, int nb, int D, int per_seq, in
     samp = t - u * ns;
 }
 
-template <int DT, bool FAST>
+constexpr int kMaxSampPairs = 4;   // chunk pairs per fused sampler in ticket order: samp_cps <= 8
+#ifndef SD_SAMP_PREFETCH
+#define SD_SAMP_PREFETCH 0            // 1: ticket-order samplers load the next chunk pair ahead (93 VGPRs: slower at B = 512)
+#endif
+template <int DT, bool FAST, int MAXP>
 __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int wg_id);
 template <int DT, bool FAST>
 __device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decision& d, uint32_t epoch, int wg_id);
@@ -470,7 +478,7 @@ __device__ __forceinline__ void fused_finish(const Plan& P, int b, const Decisio
 // P.n_samp sampling workgroups poll the decider's decision records, draw their chunk's candidate of
 // the decided row and publish it; the decider then polls those records and finishes (the token, the
 // outputs, the engine state): no k_sample launch, no kernel boundary, no decision reload.
-template <int DT, bool FAST, bool TAIL, bool SAMP>
+template <int DT, bool FAST, bool TAIL, bool SAMP, bool TICKET = false>
 __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_cnt) {
     __shared__ float lm[4], ls[4];
     constexpr int VEC = Elem<DT>::kVec;
@@ -494,7 +502,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     int b, s, chunk;
     bool decider = false;
     int samp = -1;
-    if (SAMP && P.ticket) {
+    if constexpr (SAMP && TICKET) {
         // Ticket mode (any batch; the grid need not be resident): a workgroup's work item is the
         // arrival ticket it takes, not its block id.  The sequences are dealt to `labels` labels
         // (b % labels), and a workgroup serves the label of its block id (id % labels: with labels a
@@ -530,7 +538,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
         chunk = samp < 0 && item < n_span ? item % gx : 0;
         SD_TS_ROLE(wg_id, ((int64_t)s_tk << 32) | ((int64_t)b << 12) |
                               (samp >= 0 ? 0x800 | samp : (decider ? 0x400 : item)));
-    } else if (SAMP && wg_id >= P.B * per_seq) {
+    } else if (SAMP && !TICKET && wg_id >= P.B * per_seq) {
         // the samplers come after every span and decider in dispatch order (block id): they only wait
         // for a decision, so the spans, which wait for nothing, always get their slots first, and a
         // sampler frees its slot once it has published.  Sequence b = id % B: with B % 8 == 0 every
@@ -550,7 +558,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     }
     if constexpr (SAMP) {
         if (samp >= 0) {
-            fused_sampler<DT, FAST>(P, b, samp, wg_id);
+            fused_sampler<DT, FAST, TICKET ? kMaxSampPairs : 1>(P, b, samp, wg_id);
             return;
         }
     }
@@ -673,17 +681,19 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     uint4 tailv = make_uint4(0u, 0u, 0u, 0u);
     if (vtail) tailv = ld16_clamped<DT>(row, tail_e0, last_whole_vec<DT>(P.V));
     if (nfull > 0) {
+        // ticket order (large batches): more vectors in flight per span (SD_TICKET_PIPE)
+        constexpr int PIPE = TICKET ? kTicketPipe : kPipe;
         const uint4* vb = reinterpret_cast<const uint4*>(row) + threadIdx.x;   // stage k at vb[k * kThreads]
-        uint4 buf[kPipe];
+        uint4 buf[PIPE];
 #pragma unroll
-        for (int d = 0; d < kPipe; ++d) buf[d] = vb[stage_of(d < nfull ? d : nfull - 1) * kThreads];
+        for (int d = 0; d < PIPE; ++d) buf[d] = vb[stage_of(d < nfull ? d : nfull - 1) * kThreads];
         read_epoch();
         int it = 0;
-        for (; it + kPipe <= nfull; it += kPipe) {
+        for (; it + PIPE <= nfull; it += PIPE) {
 #pragma unroll
-            for (int d = 0; d < kPipe; ++d) {
+            for (int d = 0; d < PIPE; ++d) {
                 const uint4 v = buf[d];
-                const int nx = it + d + kPipe;
+                const int nx = it + d + PIPE;
                 buf[d] = vb[stage_of(nx < nfull ? nx : nfull - 1) * kThreads];
                 float x[VEC];
                 unpack16<DT>(v, x);
@@ -691,7 +701,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
             }
         }
 #pragma unroll
-        for (int d = 0; d < kPipe; ++d) {
+        for (int d = 0; d < PIPE; ++d) {
             if (it + d < nfull) {
                 float x[VEC];
                 unpack16<DT>(buf[d], x);
@@ -773,9 +783,11 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_stats(Plan P, int slot
 #else
 #define SD_FUSED_VGPR_CAP
 #endif
-template <int DT, bool FAST>
+// TICKET: the ticket-order layout (fused_role; any batch): its own instantiation, so the block-id
+// kernel of small batches carries neither the ticket code nor the multi-chunk samplers' registers
+template <int DT, bool FAST, bool TICKET>
 __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP SD_FUSED_VGPR_CAP k_verify_fused(Plan P, int slot_lo, int slot_cnt) {
-    stats_body<DT, FAST, true, true>(P, slot_lo, slot_cnt);
+    stats_body<DT, FAST, true, true, TICKET>(P, slot_lo, slot_cnt);
 }
 
 // combine the chunk partials of row r (one wave)
@@ -2346,7 +2358,6 @@ __global__ void __launch_bounds__(kThreads) SD_SGPR_CAP k_sample(Plan P) {
 #define SD_SAMP_SLEEP 1   // fused samplers' decision poll interval (s_sleep units of 64 clocks)
 #endif
 constexpr int kFusedEpt = 8;                       // k_sample's chunking: 2048-element chunks, the same draws
-constexpr int kMaxSampPairs = 4;                   // chunk pairs per sampler: samp_cps <= 8
 
 __device__ __forceinline__ uint32_t dec_tag(uint32_t epoch, int b, int k) {
     uint32_t h = epoch * 0x9E3779B1u + (uint32_t)b * 0x85EBCA77u + (uint32_t)k * 0xC2B2AE3Du + 0x1B873593u;
@@ -2426,7 +2437,7 @@ __device__ __forceinline__ void fused_weights(const PairRows& R, int cc, int rch
     }
 }
 
-template <int DT, bool FAST>
+template <int DT, bool FAST, int MAXP>
 __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int wg_id) {
     __shared__ uint4 s_rec[2];
     __shared__ uint32_t s_ep;
@@ -2488,7 +2499,7 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     constexpr int VEC = Elem<DT>::kVec, NV = kFusedEpt / VEC;
     if (!(R.t_al && (!R.resid || R.d_al) && P.V >= VEC)) {   // misaligned rows: one chunk at a time
 #pragma unroll
-        for (int k = 0; k < kMaxSampPairs; ++k) {
+        for (int k = 0; k < MAXP; ++k) {
             const int q = q0 + k, c0 = 2 * q, c1 = 2 * q + 1;
             if (k >= nq || c0 >= P.rn_chunks) break;
             if (k > 0) {
@@ -2518,12 +2529,17 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
                 if (R.resid) d1 = ld16_clamped<DT>(R.drow, e1, lastv);
             }
         };
+        // one pair in flight ahead (ticket order: the next pair's vectors load while this pair's
+        // weights and draws run)
+        uint4 t0, d0, t1, d1;
+        ld_pair(q0, t0, d0, t1, d1);
 #pragma unroll
-        for (int k = 0; k < kMaxSampPairs; ++k) {
+        for (int k = 0; k < MAXP; ++k) {
             const int q = q0 + k, c0 = 2 * q, c1 = 2 * q + 1;
             if (k >= nq || c0 >= P.rn_chunks) break;
-            uint4 t0, d0, t1, d1;
-            ld_pair(q, t0, d0, t1, d1);
+            if (!SD_SAMP_PREFETCH && k > 0) ld_pair(q, t0, d0, t1, d1);
+            uint4 nt0 = t0, nd0 = d0, nt1 = t1, nd1 = d1;
+            if (SD_SAMP_PREFETCH && k + 1 < MAXP && k + 1 < nq && 2 * (q + 1) < P.rn_chunks) ld_pair(q + 1, nt0, nd0, nt1, nd1);
             if (k > 0) {
                 u0 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 1u + 2u * (uint32_t)q));
                 u1 = uniform_d(cdf_uniform(P.noise, (uint32_t)b, 2u + 2u * (uint32_t)q));
@@ -2536,6 +2552,7 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
                 fused_weights<DT>(R, c1, P.rchunk, e1, t1, d1, wv, psum);
                 sample_chunk_pick<DT, DT, kFusedEpt>(P, b, c1, wv, psum, sample_tag(ep, b, c1), wg_id, u1);
             }
+            t0 = nt0; d0 = nd0; t1 = nt1; d1 = nd1;
         }
         SD_TS(wg_id, 2);
         return;
@@ -2565,7 +2582,7 @@ __device__ __forceinline__ void fused_sampler(const Plan& P, int b, int c, int w
     // the general rows (fp32, processors): chunk c0's vectors, its weights, then chunk c1's loads go
     // out before c0's draw; only the weights of one chunk and the raw vectors of the other are live
 #pragma unroll
-    for (int k = 0; k < kMaxSampPairs; ++k) {
+    for (int k = 0; k < MAXP; ++k) {
         const int q = q0 + k, c0 = 2 * q, c1 = 2 * q + 1;
         if (k >= nq || c0 >= P.rn_chunks) break;
         const bool has1 = c1 < P.rn_chunks;
@@ -3124,9 +3141,10 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     auto y = [&](int k) { return lean_elem<DT>(raw, k); };
     // an empty asm that "rewrites" the packed vectors: the passes after it cannot reuse values the
     // compiler derived from them before (it would keep every unpacked element and weight live)
-    // (one stage already fits 64 VGPRs: the bench shape's draw keeps the compiler's schedule)
+    // (one or two stages fit 64 VGPRs as they are: those draws keep the compiler's schedule — the
+    // re-derived values cost the 2-stage draw 1 us at B = 128)
     auto fence_raw = [&]() {
-        if constexpr (NST > 1)
+        if constexpr (NST >= 4)
 #pragma unroll
         for (int v = 0; v < NST; ++v) asm volatile("" : "+v"(raw[v].x), "+v"(raw[v].y), "+v"(raw[v].z), "+v"(raw[v].w));
     };
@@ -3691,16 +3709,22 @@ int32_t launch_fused_dt(const sd::Plan& P, bool fast, void* stream) {
     if (!poll_allowed()) return 0;
     sd::Plan Q = P;
     Q.kpoll = 1;
-    if (fast) SD_LAUNCH((k_verify_fused<DT, true>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
-    else SD_LAUNCH((k_verify_fused<DT, false>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+    if (P.ticket) {
+        if (fast) SD_LAUNCH((k_verify_fused<DT, true, true>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+        else SD_LAUNCH((k_verify_fused<DT, false, true>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+    } else {
+        if (fast) SD_LAUNCH((k_verify_fused<DT, true, false>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+        else SD_LAUNCH((k_verify_fused<DT, false, false>), dim3((uint32_t)total), dim3(kThreads), stream, Q, 0, P.n_tslots);
+    }
     return 1;
 }
 
+// the block-id layout's kernel (its residency decides between the layouts, fused_layout)
 const void* fused_kernel(const sd::Plan& P) {
     const bool fast = P.tT == 1.0f && P.dT == 1.0f && !P.t_keep && !P.d_keep;
-    if (P.tdt == SD_BF16) return fast ? (const void*)k_verify_fused<SD_BF16, true> : (const void*)k_verify_fused<SD_BF16, false>;
-    if (P.tdt == SD_F16) return fast ? (const void*)k_verify_fused<SD_F16, true> : (const void*)k_verify_fused<SD_F16, false>;
-    return fast ? (const void*)k_verify_fused<SD_F32, true> : (const void*)k_verify_fused<SD_F32, false>;
+    if (P.tdt == SD_BF16) return fast ? (const void*)k_verify_fused<SD_BF16, true, false> : (const void*)k_verify_fused<SD_BF16, false, false>;
+    if (P.tdt == SD_F16) return fast ? (const void*)k_verify_fused<SD_F16, true, false> : (const void*)k_verify_fused<SD_F16, false, false>;
+    return fast ? (const void*)k_verify_fused<SD_F32, true, false> : (const void*)k_verify_fused<SD_F32, false, false>;
 }
 
 int32_t launch_fused(const sd::Plan& P, void* stream) {
