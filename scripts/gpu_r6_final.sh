@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-6 closing evidence (GPU box): the whole GPU suite, the default bench line, rocprofv3 kernel
 # traces of the B=32 headline step and the B=512 sweep step (--profile-only), their FETCH_SIZE /
-# WRITE_SIZE passes, and a kernel trace of the pipelined STREAM step.  Outputs under gpurun_out/;
+# WRITE_SIZE passes, a kernel trace of the pipelined STREAM step and the B = 512 ticket-order phase
+# probe (scripts/ticket_phases.py, the timing build).  Outputs under gpurun_out/;
 # every GPU step has its own time limit and the first failure ends the script.
 #   SKIP_TESTS=1 / SKIP_BENCH=1 skip those steps.
 set -eo pipefail
@@ -30,3 +31,5 @@ for B in 32 512; do
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_stream -o run -- \
   python3 $R/scripts/stream_timing.py > $R/gpurun_out/prof_stream.txt 2> $R/gpurun_out/prof_stream.log
+cd $R
+timeout -k 10 180 python scripts/ticket_phases.py > gpurun_out/ticket_phases_B512.txt 2>&1
