@@ -296,7 +296,7 @@ typedef enum {
     SD_OPT_DRAW_SPAN = 6,       /* ABI 11. 0 (default): k_draw_lean's span per workgroup chosen by
                                    the batch (2048 elements, more for large batches); 1 / 2 / 4:
                                    that many 2048-element stages per workgroup                    */
-    SD_OPT_TICKET_LAG = 7,      /* ABI 11. 0 (default, 2): in the ticket-order fused verify, how many
+    SD_OPT_TICKET_LAG = 7,      /* ABI 11. 0 (default, 1): in the ticket-order fused verify, how many
                                    sequences of a label stream before an earlier one's samplers  */
     SD_OPT_SAMP_CHUNKS = 8,     /* ABI 11. 0 (default: 2, 4 in ticket order): 2048-element chunks each
                                    sampling workgroup of the fused verify draws; 2, 4 or 8 pin it

@@ -463,6 +463,9 @@ __device__ __forceinline__ void fused_role(int t, int nb, int D, int per_seq, in
     samp = t - u * ns;
 }
 
+#ifndef SD_TAIL_PRIO
+#define SD_TAIL_PRIO 1   // s_setprio for the draws' tail wave and the fused verify's decider (B = 32 step -0.35 us)
+#endif
 constexpr int kMaxSampPairs = 4;   // chunk pairs per fused sampler in ticket order: samp_cps <= 8
 #ifndef SD_SAMP_PREFETCH
 #define SD_SAMP_PREFETCH 0            // 1: ticket-order samplers load the next chunk pair ahead (93 VGPRs: slower at B = 512)
@@ -564,6 +567,7 @@ __device__ __forceinline__ void stats_body(const Plan& P, int slot_lo, int slot_
     }
     __shared__ uint32_t s_epoch;
     if (TAIL && decider) {
+        if (SD_TAIL_PRIO) __builtin_amdgcn_s_setprio(2);   // the sequence's critical path (see k_draw_lean's tail)
         // the drafts' ids, logits, drafter stats, stop flags and accept uniforms while the spans stream
         DraftPf pf;
         const int pi = pf_draft(P);
@@ -1028,6 +1032,19 @@ __device__ int64_t walk_seq(const Plan& P, int b, int64_t woff) {
     return used;
 }
 
+// The walk's accept tests on the raw words: torch.rand's u = m 2^-24, m = word & 0xffffff (exact in
+// fp32), so u < t (ENGINE, accept_draft) is m < ceil(t 2^24) and !(u > t) (SPEC, a NaN t accepts) is
+// m < floor(t 2^24) + 1 — t 2^24 is exact in fp64 — clamped to [0, 2^24].  The serial chain then
+// compares integers (it converted each word and compared in fp64).
+__device__ __forceinline__ uint32_t walk_thr_word(bool spec, double t) {
+    constexpr double k24 = 16777216.0;
+    if (t != t) return spec ? (1u << 24) : 0u;
+    if (spec ? !(t >= 0.0) : !(t > 0.0)) return 0u;
+    if (t >= 1.0) return 1u << 24;
+    const double x = t * k24;
+    return (uint32_t)(spec ? floor(x) + 1.0 : ceil(x));
+}
+
 // STREAM k_walk's LDS budget: the uniform windows of a block of rows (words), and the block's
 // per-draft inputs (rows x gamma)
 constexpr int kWalkWords = 12288;
@@ -1047,7 +1064,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
         //   3. every row's decision is rebuilt from its (a, k) and published in parallel.
         // (Before: one dependent global round trip per row, ~3 us each.)
         __shared__ uint32_t lw[kWalkWords];
-        __shared__ double lthr[kWalkDrafts];
+        __shared__ uint32_t lthr[kWalkDrafts];   // accept iff (word & 0xffffff) < lthr (walk_thr_word)
         __shared__ float lrp[kWalkDrafts], lrq[kWalkDrafts];
         __shared__ uint8_t lstop[kWalkDrafts], lact[kWalkDrafts];
         __shared__ int32_t la[kWalkDrafts], lk[kWalkDrafts];
@@ -1072,21 +1089,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                 // per load), the drafts' p/q, ids and the rows' active flags — then the LDS writes
                 // (a load behind a per-load branch, or a loop of load -> store pairs, paid one round
                 // trip each)
-                constexpr int kPer = kWalkWords / 256;
-                const float invW = 1.0f / (float)W;
-                const int nw = nb * W;
-                const uint32_t* pw = stream_ptr(P.noise);
-                const int64_t pcap = stream_cap(P.noise);
-                uint32_t wv[kPer];
-#pragma unroll
-                for (int q = 0; q < kPer; ++q) {
-                    const int i = tid + q * 256;
-                    const int k = (int)(((float)i + 0.5f) * invW), j = i - k * W;   // exact: i, W < 2^14
-                    const int64_t w = off + V2 * k + j;
-                    const bool ok = i < nw && w < pcap;
-                    wv[q] = pw[ok ? w : 0];
-                    wv[q] = ok ? wv[q] : 0u;
-                }
+                // the drafts' inputs first: in flight with the windows' first round
                 constexpr int kPerD = kWalkDrafts / 256;
                 float rp[kPerD], rq[kPerD];
                 int64_t tok[kPerD];
@@ -1101,9 +1104,53 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                     tok[q] = P.draft_tokens[b * P.tok_stride + (i < W ? d : 0)];
                     act[q] = P.active == nullptr ? 1 : P.active[b] != 0;
                 }
+                // The nb windows are W-word runs 2V words apart: each is read as nv aligned 16-byte
+                // vectors (the first and last partly outside it; its own shift sh, as 2V words need
+                // not be a multiple of 4), eight per thread per round, all in flight before their
+                // words go to LDS.  Vectors that reach past the words the call may read (stream_cap)
+                // take guarded word loads.
+                const uint32_t* pw = stream_ptr(P.noise);
+                const int64_t pcap = stream_cap(P.noise);
+                const int sh0 = (int)((reinterpret_cast<uintptr_t>(pw + off) >> 2) & 3);   // window 0's shift
+                const int nv = (W + 6) >> 2;   // covers W words after any shift <= 3
+                const float invNv = 1.0f / (float)nv;
+                const int nvec = nb * nv;
+                constexpr int kVr = 8;
+                for (int r0 = 0; r0 < nvec; r0 += kVr * 256) {
+                    uint4 vv[kVr];
+                    int kq[kVr], jq[kVr];
+                    int64_t wq[kVr];
 #pragma unroll
-                for (int q = 0; q < kPer; ++q)
-                    if (tid + q * 256 < nw) lw[tid + q * 256] = wv[q];
+                    for (int q = 0; q < kVr; ++q) {
+                        const int t = r0 + tid + q * 256;
+                        const int tc = t < nvec ? t : nvec - 1;
+                        const int k = (int)(((float)tc + 0.5f) * invNv), v = tc - k * nv;   // exact: tc, nv < 2^14
+                        const int sh = (sh0 + (int)((V2 * k) & 3)) & 3;        // window k's shift
+                        const int64_t w0 = off + V2 * k + 4 * v - sh;      // the vector's first word
+                        kq[q] = t < nvec ? k : -1;
+                        jq[q] = 4 * v - sh;
+                        // unconditional loads (a vector outside the readable words reads the pool's
+                        // first one instead and is patched below, word by word)
+                        wq[q] = w0;
+                        const bool whole = w0 >= 0 && w0 + 4 <= pcap;
+                        vv[q] = *reinterpret_cast<const uint4*>(whole ? pw + w0 : P.noise.words);
+                    }
+#pragma unroll
+                    for (int q = 0; q < kVr; ++q) {
+                        if (kq[q] < 0) continue;
+                        uint32_t e[4] = {vv[q].x, vv[q].y, vv[q].z, vv[q].w};
+                        const int64_t w0 = wq[q];
+                        if (!(w0 >= 0 && w0 + 4 <= pcap)) {   // the readable words' edge (rare)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) e[c] = w0 + c >= 0 && w0 + c < pcap ? pw[w0 + c] : 0u;
+                        }
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const int j = jq[q] + c;
+                            if (j >= 0 && j < W) lw[kq[q] * W + j] = e[c];
+                        }
+                    }
+                }
 #pragma unroll
                 for (int q = 0; q < kPerD; ++q) {
                     const int i = tid + q * 256;
@@ -1112,7 +1159,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                     lrp[i] = p;
                     lrq[i] = qq;
                     // accept iff u <= p/q (fp32, SPEC) / u < min(1, p/q) (fp64, ENGINE): accept_draft's rules
-                    lthr[i] = spec ? (double)(p / qq) : ((double)qq <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)qq));
+                    lthr[i] = walk_thr_word(spec, spec ? (double)(p / qq) : ((double)qq <= 0.0 ? 1.0 : fmin(1.0, (double)p / (double)qq)));
                     uint32_t r8 = 0;   // stop_rank8 from the staged list
                     if (lds_stops) {
                         for (int k = P.n_stop - 1; k >= 0; --k)
@@ -1138,30 +1185,34 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                 // the chain)
                 int a = 0, k = 0, my_a = 0, my_k = 0;
                 const bool in = lane < g;
-                double t = lthr[in ? lane : 0];
+                const bool t_stoch = P.t_stoch != 0;
+                uint32_t t = lthr[in ? lane : 0];
                 uint64_t stp = lstpm[0];
                 bool ract = lact[0] != 0;
                 for (int bi = 0; bi < nb; ++bi) {
-                    const float u = uniform_from_word(lw[k * W + a + (in ? lane : 0)]);
+                    const uint32_t m = lw[k * W + a + (in ? lane : 0)] & 0xFFFFFFu;   // u = m 2^-24
                     const int bn = bi + 1 < nb ? bi + 1 : bi;
-                    const double t_n = lthr[bn * g + (in ? lane : 0)];
+                    const uint32_t t_n = lthr[bn * g + (in ? lane : 0)];
                     const uint64_t stp_n = lstpm[bn];
                     const bool ract_n = lact[bn * g] != 0;
                     if (bi < kWave && lane == bi) { my_a = a; my_k = k; }
                     if (bi >= kWave && lane == 0) { la[bi] = a; lk[bi] = k; }
-                    const bool acc = spec ? !((double)u > t) : (double)u < t;
+                    const bool acc = m < t;
                     const uint64_t rej = __ballot(in && !acc);
                     const int f = rej ? __builtin_ctzll(rej) : g;              // first rejected draft
                     const uint64_t before = f >= 64 ? ~0ull : ((1ull << f) - 1ull);
                     const uint64_t stop_acc = stp & before;
-                    if (spec) {
-                        a += g;
-                        k += (P.t_stoch && !stop_acc) ? 1 : 0;
-                    } else if (ract) {
-                        if (stop_acc) a += __builtin_ctzll(stop_acc) + 1;      // finished on an end token
-                        else if (f < g) { a += f + 1; k += 1; }                  // rejected: the residual row
-                        else a += g;
-                    }
+                    // the row's outcome as selects, no branch on the chain: SPEC draws g uniforms and
+                    // (stochastic rows, no stop among the accepted) one residual / bonus row; the
+                    // ENGINE's active row stops at an accepted end token, or at the first rejection
+                    // (+ the residual row), else takes all g
+                    const int stop_i = stop_acc ? (int)__builtin_ctzll(stop_acc) : g;
+                    const int da_e = stop_acc ? stop_i + 1 : (f < g ? f + 1 : g);
+                    const int dk_e = !stop_acc && f < g ? 1 : 0;
+                    const int da = spec ? g : (ract ? da_e : 0);
+                    const int dk = spec ? (t_stoch && !stop_acc ? 1 : 0) : (ract ? dk_e : 0);
+                    a += da;
+                    k += dk;
                     t = t_n;
                     stp = stp_n;
                     ract = ract_n;
@@ -1179,8 +1230,7 @@ __global__ void __launch_bounds__(256) k_walk(Plan P) {
                 bool ovr = false;
                 int64_t used;
                 for (int i = 0; i < g; ++i) {
-                    const float u = uniform_from_word(lw[lk[bi] * W + la[bi] + i]);
-                    if (spec ? !((double)u > lthr[bi * g + i]) : (double)u < lthr[bi * g + i]) accm |= 1ull << i;
+                    if ((lw[lk[bi] * W + la[bi] + i] & 0xFFFFFFu) < lthr[bi * g + i]) accm |= 1ull << i;
                 }
                 Decision d = walk_core(P, b, lrp + bi * g, lrq + bi * g, woff, &used, true, accm, lstop + bi * g);
                 const bool sampled = spec ? (d.mode != kModeNone && P.t_stoch) : d.mode == kModeResid;
@@ -3293,6 +3343,9 @@ __global__ void __launch_bounds__(kThreads) k_draw_lean(DrawLean A) {
     }
 
     // ---- tail (one wave): every span's partial, M, S, the span pick, the outputs
+    // (SD_TAIL_PRIO: the row's one latency-critical wave wins VALU issue over the co-resident
+    // producers' compute bursts — priority first, then age, MI355X_MICROARCH.md)
+    if (SD_TAIL_PRIO) __builtin_amdgcn_s_setprio(3);
     const float2* pr = reinterpret_cast<const float2*>(A.part + (int64_t)r * A.pstride);
     float M = -INFINITY;
     float mk[2], sk[2], yk[2];
@@ -3531,7 +3584,9 @@ void policy_init() {
 // Dispatch options (sd_set_option), indexed by sd_option; relaxed reads on every call.
 std::atomic<int> g_opt_fused{1}, g_opt_lean{-1}, g_opt_thr_poll{1}, g_opt_draw_stream{1}, g_opt_ticket{-1};
 std::atomic<int> g_opt_draw_span{0}, g_opt_ticket_lag{0}, g_opt_samp_chunks{0};
-constexpr int kDrawSpan2MinB = 64, kDrawSpan4MinB = 256;   // k_draw_lean: batches above take 2 / 4 stages
+// k_draw_lean: batches above kDrawSpan4MinB take 4 stages per workgroup (measured round 6, packed
+// registers: B = 128 one stage 12.9 us, two 13.7, four 13.3; B = 512 four 33.5, one 38.7)
+constexpr int kDrawSpan4MinB = 128;
 std::atomic<int>* option_slot(int32_t opt) {
     switch (opt) {
         case SD_OPT_DRAW_SPAN: return &g_opt_draw_span;
@@ -3744,7 +3799,7 @@ int32_t launch_fused(const sd::Plan& P, void* stream) {
 // false: no fused launch for this batch.
 constexpr int kTicketMinB = 64;
 constexpr int kTicketLabels = 64;   // labels (ticket counters) from B = 64; 8 below
-constexpr int kTicketLag = 2;       // default lag (SD_OPT_TICKET_LAG pins it)
+constexpr int kTicketLag = 1;       // default lag (SD_OPT_TICKET_LAG pins it): B = 512 verify 173 us at 1, 179 at 2, 185 at 3
 constexpr int kTicketSampChunks = 4;   // chunks per sampler in ticket order (SD_OPT_SAMP_CHUNKS pins it): 4 measured best at B = 128 / 512
 constexpr int kTicketSpan = 16 * kThreads * 8;   // 32768 elements: 4 spans per Llama-3 row
 bool fused_layout(sd::Plan& F) {
@@ -4040,7 +4095,7 @@ int32_t launch_draw(sd::Plan& P, void* stream) {
             // workgroups; a large batch takes 2 or 4 stages per workgroup, so each holds more bytes
             // in flight and the grid stays a few resident rounds (SD_OPT_DRAW_SPAN pins it)
             int nst = opt(g_opt_draw_span);
-            if (nst == 0) nst = P.B <= kDrawSpan2MinB ? 1 : (P.B <= kDrawSpan4MinB ? 2 : 4);
+            if (nst == 0) nst = P.B <= kDrawSpan4MinB ? 1 : 4;
             int32_t st;
             if (nst == 4) st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 4>(P, stream) : launch_draw_lean_t<SD_F16, 4>(P, stream);
             else if (nst == 2) st = P.tdt == SD_BF16 ? launch_draw_lean_t<SD_BF16, 2>(P, stream) : launch_draw_lean_t<SD_F16, 2>(P, stream);
